@@ -1,0 +1,185 @@
+"""Benchmark of the hot path: batched tracking-QP solves on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--cpu-seconds S]
+
+A step = one launch of the batched solver over the config's ego batch (C2: trajectory1,
+N=20, B=4096 per GPU, seed 2; inputs resident in HBM).  Multi-GPU (torchrun, one rank per GPU,
+RCCL): each rank solves its own contiguous shard of the same ego stream (weak scaling, no
+data-path collective); timing = max over ranks.  Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd")
+sys.path[:0] = [PKG, os.path.join(ROOT, "oracle")]
+
+FP64_PEAK_TFLOPS = 78.6     # MI355X dense FP64 (vector == matrix), MI355X_MICROARCH / AMD spec
+HBM_PEAK_GBS = 8000.0
+
+
+def algorithmic_flops(N, K):
+    """F = 20N^2 + 24N^3 + K(48N^3 + 8N^3/3 + 64N^2)  (dense condensed-PDIP count)."""
+    return 20 * N ** 2 + 24 * N ** 3 + K * (48 * N ** 3 + 8 * N ** 3 / 3 + 64 * N ** 2)
+
+
+def algorithmic_bytes(N, max_obs):
+    """x0 40 + obstacles 16*max_obs + n_obs 4 ; u0 16 + U 16N + pred_X 40(N+1) + status/iters 8."""
+    return 40 + 16 * max_obs + (4 if max_obs else 0) + 16 + 16 * N + 40 * (N + 1) + 8
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import __graft_entry__ as ge
+    ge.build()
+    import mpcqp
+    import workloads as W
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (libmpcqp has no CPU backend)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+
+    cfg = W.CONFIGS[args.config]
+    B = args.batch or cfg["B"] // max(1, cfg["gpus"])
+    wb = W.make_batch(args.config, B=B, offset=rank * B)
+    N, mo = wb["N"], wb["max_obs"]
+    X, U = W.loader(wb["traj"]).X_ref, W.loader(wb["traj"]).U_ref
+    slv = mpcqp.Solver(X, U, mpcqp.default_params(N=N, max_obs=mo), device=local)
+
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    x0 = t(wb["x0"])
+    obs = t(wb["obs"]) if wb["obs"] is not None else None
+    nob = t(wb["n_obs"], torch.int32) if wb["n_obs"] is not None else None
+    u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
+    Uo = torch.empty((B, N, 2), dtype=torch.float64, device=dev)
+    Xo = torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    ptr = lambda x: 0 if x is None else x.data_ptr()
+
+    def step():
+        slv.solve_batch_device(B, ptr(x0), ptr(obs), ptr(nob), 0, ptr(u0), ptr(Uo), ptr(Xo), ptr(st), ptr(it),
+                               stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(args.steps):
+        step()
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)])
+    gpu_s = float(step_ms.sum()) / 1e3
+    elapsed = max(wall, gpu_s)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    iters = it.cpu().numpy()
+    status = st.cpu().numpy()
+    kmean = float(iters.mean())
+    avg_launch_s = gpu_s / args.steps
+    flops = algorithmic_flops(N, kmean) * B
+    nbytes = algorithmic_bytes(N, mo) * B
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_hbm_bytes.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(args.config)
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "tracking-QP solves/sec @ N=20, batch=4096; p50 solve latency",
+            "value": world * B * args.steps / elapsed,
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "p50_batch_latency_ms": float(np.median(step_ms)),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"{args.config}: trajectory{wb['traj']}.json, N={N}, batch={B} egos per GPU, "
+                                   f"max_obs={mo}, seed {cfg['seed']} (SURVEY 8d)", "global_batch": world * B,
+                       "horizon": N, "parallelism": f"dp{world} (ego shards)"},
+            "solver": {"mean_iters": kmean, "max_iters": int(iters.max()),
+                       "status_counts": {mpcqp.STATUS_NAMES[k]: int((status == k).sum()) for k in range(4)}},
+            "roofline": {"bound": "mfma", "achieved": flops / avg_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": flops / avg_launch_s / 1e12 / FP64_PEAK_TFLOPS,
+                         "traffic": traffic,
+                         "note": "FP64 compute; achieved = SURVEY 8(d) dense-condensed flop count F(N, mean iters) "
+                                 "x B / avg launch time (HIP events on the launch stream)",
+                         "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
+        }
+        if not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(wb, N, mo, budget_s):
+    """The oracle's C restatement (same QP, same PDIP), OpenMP over the host cores, on a bounded
+    sample of the same egos.  kind = 'port' (the reference itself never travels to the GPU box)."""
+    import numpy as np
+    import oracle as O
+    import workloads as W
+    ld = W.loader(wb["traj"])
+    orc = O.Oracle(ld.X_ref, ld.U_ref)
+    p = O.default_params(N=N, max_obs=mo)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    n = min(512, wb["x0"].shape[0])
+    sl = slice(0, n)
+    obs = None if wb["obs"] is None else wb["obs"][sl]
+    nob = None if wb["n_obs"] is None else wb["n_obs"][sl]
+    orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)        # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)
+        done += n
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by the oracle's C PDIP "
+                      f"(oracle/mpc_oracle.c) with OpenMP"}
+
+
+if __name__ == "__main__":
+    main()

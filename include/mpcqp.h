@@ -1,0 +1,117 @@
+/*
+ * mpcqp.h — C ABI of the MI355X batched tracking-MPC solver (libmpcqp.so).
+ *
+ * Drop-in boundary for the reference's hot path:
+ *   TrajectoryTracker.solve(x0, obstacles) -> (u0, pred_X, solve_time)
+ *       medinammartin3/Safe-Autonomous-Driving-MPC  trajectory_tracking.py:213-263
+ *   with its read-only state: TrajectoryTracker.__init__ params  (trajectory_tracking.py:12-47)
+ *   and the reference signal  TrajectoryLoader                  (trajectory_loader.py:13-102).
+ *
+ * A reference-side binding (ctypes) is shown in INTEGRATION.md; the package's
+ * trajectory_tracking.py is that binding.
+ *
+ * Conventions
+ *   - all arrays are plain row-major float64 / int32, caller-owned;
+ *   - per-instance solver outcomes go to status[] and never fail the call
+ *     (the reference ignores SLSQP's status, trajectory_tracking.py:260-263);
+ *   - API misuse returns a negative MPC_E* code and sets mpc_last_error();
+ *   - a context is bound to one HIP device and is not re-entrant.
+ *   - There is no CPU backend: mpc_create fails loudly (MPC_E_DEVICE) without a GPU.
+ */
+#ifndef MPCQP_H
+#define MPCQP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCQP_VERSION 1
+#define MPC_MAX_N 63          /* horizon limit (one lane per stage k=0..N in the kernel)   */
+#define MPC_MAX_OBS 64        /* obstacle slab limit per instance                            */
+
+/* status[] codes */
+#define MPC_OK 0              /* QP solved to tolerance, hard constraints satisfied          */
+#define MPC_MAX_ITER 1        /* iteration limit hit; best iterate returned                  */
+#define MPC_INFEASIBLE 2      /* solved, but elastic slack active: hard QP(ubar) infeasible  */
+#define MPC_NUMERICAL 3       /* numerical breakdown; best iterate returned                  */
+
+/* return codes */
+#define MPC_SUCCESS 0
+#define MPC_E_ARG (-1)
+#define MPC_E_DEVICE (-2)
+#define MPC_E_ALLOC (-3)
+#define MPC_E_LAUNCH (-4)
+
+/* Mirrors TrajectoryTracker.__init__ (trajectory_tracking.py:17-47) plus solver knobs.
+ * Field names follow the reference attributes.  mpc_default_params() fills the reference values. */
+typedef struct mpc_params {
+    int N;                          /* horizon                      :18 (reference default 5)  */
+    int max_obs;                    /* obstacle slab width per instance in the batch arrays    */
+    double dt;                      /* control period               :17                        */
+    double u_min[2], u_max[2];      /* (u1 curvature rate, u2 accel) bounds   :31-32           */
+    double vehicle_radius;          /* :33 */
+    double w_d, w_o, w_v, w_u1, w_u2;  /* :36-40 */
+    double obstacle_safety_distance;   /* :43 */
+    double max_time_2_obs;          /* :44 */
+    double wheelbase;               /* :45 */
+    double lane_width;              /* :46 */
+    double safe_lane_margin;        /* :47 */
+    double brake_distance;          /* warm start: obstacle closer than this -> brake (:232, 40.0)  */
+    double brake_accel;             /* warm start braking control u2 (:240, -2.0)                    */
+    /* solver */
+    int linearization;              /* 1 = Gauss-Newton (reference slopes, default), 0 = frozen refs  */
+    int sqp_iters;                  /* QP solves per call: 1 = single QP at ubar (parity gate);
+                                       0 = no solve: U = ubar, Xpred = predict(x0, ubar)              */
+    int max_iter;                   /* PDIP iteration cap per QP                                     */
+    int polish;                     /* 1 = active-set polish of the interior-point result (default)   */
+    double tol;                     /* relative primal/dual residual tolerance                        */
+    double tol_mu;                  /* absolute complementarity tolerance                             */
+    double elastic_rho;             /* L1 penalty of the elastic (soft) state rows                    */
+} mpc_params;
+
+typedef struct mpc_ctx mpc_ctx;
+
+/* Fill p with the reference values of trajectory_tracking.py:17-47 (N=5) and solver defaults. */
+void mpc_default_params(mpc_params* p);
+
+/* Create a context on HIP device `device`.  X: T x 5 reference states (s,d,o,k,v), U: Tu x 2
+ * reference controls, exactly the arrays of the trajectory JSON (trajectory_loader.py:22-24);
+ * the strict-monotone s fix of trajectory_loader.py:26-30 is applied here.  The table is copied
+ * to device memory (owned by the context).  Replaces TrajectoryLoader(...) + TrajectoryTracker(X_ref). */
+int mpc_create(const double* X, int T, const double* U, int Tu, const mpc_params* p, int device,
+               mpc_ctx** out);
+
+/* Batched TrajectoryTracker.solve (trajectory_tracking.py:213-263), host buffers, synchronous.
+ *   x0     [B][5]              current states
+ *   obs    [B][max_obs][2]     (s, v) of each obstacle; may be NULL if max_obs == 0
+ *   n_obs  [B]                 obstacles used per instance (<= max_obs); may be NULL
+ *   ubar   [B][N][2] or NULL   linearization point; NULL = the reference warm start (:224-246)
+ * outputs (any may be NULL):
+ *   u0 [B][2], U [B][N][2], Xpred [B][N+1][5] (nonlinear predict(x0,U*), :261),
+ *   status [B], iters [B]  */
+int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, const int* n_obs,
+                    const double* ubar, double* u0, double* U, double* Xpred, int* status, int* iters);
+
+/* Same, with device pointers, launched asynchronously on `stream` (a hipStream_t; 0 = null stream).
+ * No host synchronisation, no allocation (graph-capturable). */
+int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const double* obs, const int* n_obs,
+                           const double* ubar, double* u0, double* U, double* Xpred, int* status,
+                           int* iters, void* stream);
+
+/* Reference-signal service on the device table: TrajectoryLoader.get_state / get_control
+ * (trajectory_loader.py:86-102), batched. Host buffers, synchronous.  out_state [n][5], out_control [n][2]. */
+int mpc_lookup(mpc_ctx* c, int n, const double* s, double* out_state, double* out_control);
+
+/* Change parameters of an existing context (e.g. TrajectoryTracker.N = 20 after construction). */
+int mpc_set_params(mpc_ctx* c, const mpc_params* p);
+int mpc_get_params(const mpc_ctx* c, mpc_params* p);
+
+/* Thread-local description of the last API error on this thread. */
+const char* mpc_last_error(void);
+int mpc_version(void);
+void mpc_destroy(mpc_ctx* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCQP_H */

@@ -1,0 +1,166 @@
+"""ctypes binding of libmpcqp.so (include/mpcqp.h) — the MI355X batched tracking-MPC solver.
+
+This is the product's host boundary.  It loads the in-tree HIP library and fails loudly when
+it is missing or when no GPU is present: there is no CPU fallback (the CPU restatement in
+oracle/ is test infrastructure and is never used here).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmpcqp.so")
+
+MPC_OK, MPC_MAX_ITER, MPC_INFEASIBLE, MPC_NUMERICAL = 0, 1, 2, 3
+STATUS_NAMES = {0: "ok", 1: "max_iter", 2: "infeasible", 3: "numerical"}
+MAX_N = 63
+MAX_OBS = 64
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+
+class MpcParams(C.Structure):
+    """`mpc_params` of include/mpcqp.h (mirrors TrajectoryTracker.__init__, trajectory_tracking.py:17-47)."""
+    _fields_ = [
+        ("N", C.c_int), ("max_obs", C.c_int), ("dt", C.c_double),
+        ("u_min", C.c_double * 2), ("u_max", C.c_double * 2),
+        ("vehicle_radius", C.c_double),
+        ("w_d", C.c_double), ("w_o", C.c_double), ("w_v", C.c_double), ("w_u1", C.c_double), ("w_u2", C.c_double),
+        ("obstacle_safety_distance", C.c_double), ("max_time_2_obs", C.c_double), ("wheelbase", C.c_double),
+        ("lane_width", C.c_double), ("safe_lane_margin", C.c_double),
+        ("brake_distance", C.c_double), ("brake_accel", C.c_double),
+        ("linearization", C.c_int), ("sqp_iters", C.c_int), ("max_iter", C.c_int), ("polish", C.c_int),
+        ("tol", C.c_double), ("tol_mu", C.c_double), ("elastic_rho", C.c_double),
+    ]
+
+
+class MpcError(RuntimeError):
+    pass
+
+
+EXPORTS = ["mpc_default_params", "mpc_create", "mpc_solve_batch", "mpc_solve_batch_device", "mpc_lookup",
+           "mpc_set_params", "mpc_get_params", "mpc_last_error", "mpc_version", "mpc_destroy"]
+
+_lib = None
+
+
+def lib():
+    """Load libmpcqp.so (raises if it has not been built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpcError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    L.mpc_default_params.argtypes = [C.POINTER(MpcParams)]
+    L.mpc_create.restype = C.c_int
+    L.mpc_create.argtypes = [_dp, C.c_int, _dp, C.c_int, C.POINTER(MpcParams), C.c_int, C.POINTER(C.c_void_p)]
+    L.mpc_solve_batch.restype = C.c_int
+    L.mpc_solve_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _ip, _dp, _dp, _dp, _dp, _ip, _ip]
+    L.mpc_solve_batch_device.restype = C.c_int
+    L.mpc_solve_batch_device.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mpc_lookup.restype = C.c_int
+    L.mpc_lookup.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp]
+    L.mpc_set_params.restype = C.c_int
+    L.mpc_set_params.argtypes = [C.c_void_p, C.POINTER(MpcParams)]
+    L.mpc_get_params.restype = C.c_int
+    L.mpc_get_params.argtypes = [C.c_void_p, C.POINTER(MpcParams)]
+    L.mpc_last_error.restype = C.c_char_p
+    L.mpc_version.restype = C.c_int
+    L.mpc_destroy.argtypes = [C.c_void_p]
+    _lib = L
+    return L
+
+
+def last_error():
+    return lib().mpc_last_error().decode()
+
+
+def default_params(**kw):
+    p = MpcParams()
+    lib().mpc_default_params(C.byref(p))
+    for k, v in kw.items():
+        if k in ("u_min", "u_max"):
+            arr = getattr(p, k)
+            arr[0], arr[1] = float(v[0]), float(v[1])
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def _pi(a):
+    return None if a is None else a.ctypes.data_as(_ip)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise MpcError(f"{what} failed (rc={rc}): {last_error()}")
+
+
+class Solver:
+    """One libmpcqp context: device-resident reference table + parameters (one HIP device)."""
+
+    def __init__(self, X, U, params=None, device=0):
+        self.X = np.ascontiguousarray(X, np.float64)
+        self.U = np.ascontiguousarray(U, np.float64)
+        if self.X.ndim != 2 or self.X.shape[1] != 5 or self.U.ndim != 2 or self.U.shape[1] != 2:
+            raise ValueError("X must be [T,5] and U [Tu,2]")
+        self.params = params if params is not None else default_params()
+        h = C.c_void_p()
+        _check(lib().mpc_create(_p(self.X), self.X.shape[0], _p(self.U), self.U.shape[0], C.byref(self.params),
+                                int(device), C.byref(h)), "mpc_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().mpc_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, params):
+        _check(lib().mpc_set_params(self.h, C.byref(params)), "mpc_set_params")
+        self.params = params
+
+    def solve_batch(self, x0, obs=None, n_obs=None, ubar=None):
+        """x0 [B,5]; obs [B,max_obs,2] (s, v); n_obs [B]; ubar [B,N,2] or None (reference warm start).
+        Returns dict(u0 [B,2], U [B,N,2], Xpred [B,N+1,5], status [B], iters [B])."""
+        p = self.params
+        N, mo = p.N, p.max_obs
+        x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 5)
+        B = x0.shape[0]
+        if obs is not None and mo > 0:
+            obs = np.ascontiguousarray(obs, np.float64).reshape(B, mo, 2)
+            n_obs = (np.full(B, mo, np.int32) if n_obs is None
+                     else np.ascontiguousarray(n_obs, np.int32).reshape(B))
+        else:
+            obs, n_obs = None, None
+        ub = None if ubar is None else np.ascontiguousarray(ubar, np.float64).reshape(B, N, 2)
+        u0 = np.empty((B, 2)); U = np.empty((B, N, 2)); X = np.empty((B, N + 1, 5))
+        st = np.empty(B, np.int32); it = np.empty(B, np.int32)
+        _check(lib().mpc_solve_batch(self.h, B, _p(x0), _p(obs), _pi(n_obs), _p(ub), _p(u0), _p(U), _p(X), _pi(st),
+                                     _pi(it)), "mpc_solve_batch")
+        return dict(u0=u0, U=U, Xpred=X, status=st, iters=it)
+
+    def solve_batch_device(self, B, x0_ptr, obs_ptr, nobs_ptr, ubar_ptr, u0_ptr, U_ptr, X_ptr, st_ptr, it_ptr,
+                           stream=0):
+        """Device-pointer variant (ints are raw device addresses, e.g. torch tensor.data_ptr())."""
+        _check(lib().mpc_solve_batch_device(self.h, int(B), x0_ptr, obs_ptr, nobs_ptr, ubar_ptr, u0_ptr, U_ptr,
+                                            X_ptr, st_ptr, it_ptr, C.c_void_p(stream)), "mpc_solve_batch_device")
+
+    def lookup(self, s):
+        s = np.ascontiguousarray(s, np.float64).ravel()
+        st = np.empty((s.size, 5)); ct = np.empty((s.size, 2))
+        _check(lib().mpc_lookup(self.h, s.size, _p(s), _p(st), _p(ct)), "mpc_lookup")
+        return st, ct

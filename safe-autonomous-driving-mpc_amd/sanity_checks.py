@@ -1,0 +1,81 @@
+"""trajectory_tracking_check — restated acceptance checks over closed-loop telemetry.
+
+Same checks, tolerances and prints as sanity_checks.py:79-184 of the reference
+(destination within 1 m, |d| <= 1.5 m, controls within bounds +-0.1, max solve time <= 150 ms,
+dynamic-obstacle gap >= 1 m, no RED-light pass).  Returns the bool like the reference.
+`check_summary` is the silent, structured form used by the batched closed loop and the bench.
+"""
+import numpy as np
+
+LATERAL_LIMIT = 1.5
+CONTROLS_TOL = 0.1
+CPU_LIMIT = 150      # ms
+SAFETY_DIST = 1.0
+
+
+def check_summary(u_min, u_max, hist_x, hist_u, hist_t, hist_obs_s, hist_tl_red, dynamic_obstacle,
+                  traffic_light, tl_pos, s_total):
+    """All checks of sanity_checks.py:79-184 as a dict of bools (+ the measured quantities)."""
+    hist_x = np.asarray(hist_x, np.float64)
+    hist_u = np.asarray(hist_u, np.float64)
+    hist_t = np.asarray(hist_t, np.float64)
+    out = {}
+    out["s_final"] = float(hist_x[-1, 0])
+    out["destination"] = not (out["s_final"] < s_total - 1.0)                          # :97-103
+    out["max_dev"] = float(np.max(np.abs(hist_x[:, 1])))
+    out["on_road"] = not (out["max_dev"] > LATERAL_LIMIT)                              # :105-111
+    u1, u2 = hist_u[:, 0], hist_u[:, 1]
+    out["steer_ok"] = not ((np.min(u1) < u_min[0] - CONTROLS_TOL) or (np.max(u1) > u_max[0] + CONTROLS_TOL))
+    out["accel_ok"] = not ((np.min(u2) < u_min[1] - CONTROLS_TOL) or (np.max(u2) > u_max[1] + CONTROLS_TOL))
+    out["max_cpu_ms"] = float(np.max(hist_t) * 1000) if hist_t.size else 0.0
+    out["realtime"] = not (out["max_cpu_ms"] > CPU_LIMIT)                             # :133-139
+    out["obstacle_ok"] = True
+    out["min_obs_dist"] = float("nan")
+    if dynamic_obstacle:                                                              # :141-161
+        obs_s = np.asarray(hist_obs_s, np.float64)
+        valid = ~np.isnan(obs_s)
+        if np.any(valid):
+            m = min(len(hist_x), len(obs_s))
+            d = obs_s[:m][valid[:m]] - hist_x[:m, 0][valid[:m]]
+            out["min_obs_dist"] = float(np.min(d))
+            out["obstacle_ok"] = not (out["min_obs_dist"] < SAFETY_DIST)
+    out["light_ok"] = True
+    if traffic_light:                                                                 # :163-181
+        idx = np.where(hist_x[:, 0] > tl_pos)[0]
+        if len(idx) > 0 and idx[0] < len(hist_tl_red) and bool(hist_tl_red[idx[0]]):
+            out["light_ok"] = False
+    out["passed"] = all(out[k] for k in ("destination", "on_road", "steer_ok", "accel_ok", "realtime",
+                                         "obstacle_ok", "light_ok"))
+    return out
+
+
+def trajectory_tracking_check(tracker, hist_x, hist_u, hist_t, hist_obs_s, hist_tl_state, fsm, s_total):
+    """Verifies safety, performance and real-time constraints of a tracking run (prints like the reference)."""
+    print("\n=== SANITY CHECKS ===")
+    red = [s == "RED" for s in hist_tl_state]
+    r = check_summary(tracker.u_min, tracker.u_max, hist_x, hist_u, hist_t, hist_obs_s, red,
+                      fsm.dynamic_obstacle, fsm.traffic_light, getattr(fsm, "tl_pos", 0.0), s_total)
+    if not r["destination"]:
+        print(f'Destination reached : False --> Stopped at {r["s_final"]:.1f}/{s_total:.1f} m')
+    else:
+        print('Destination reached : True')
+    if not r["on_road"]:
+        print(f'Stayed on road : False --> Max Deviation = {r["max_dev"]:.2f} m')
+    else:
+        print('Stayed on road : True')
+    print(f'Steering controls within limits : {r["steer_ok"]}')
+    print(f'Acceleration controls within limits : {r["accel_ok"]}')
+    if not r["realtime"]:
+        print(f'Real-time constraint respected : False --> Max CPU time {r["max_cpu_ms"]:.1f}ms > {CPU_LIMIT}ms')
+    else:
+        print('Real-time constraint respected : True')
+    if fsm.dynamic_obstacle and not np.isnan(r["min_obs_dist"]):
+        if not r["obstacle_ok"]:
+            print(f'Dynamic Obstacle Avoided : False --> Min Distance = {r["min_obs_dist"]:.2f} m')
+        else:
+            print('Dynamic Obstacle Avoided : True')
+    if fsm.traffic_light:
+        print('Traffic Light Respected : False (Ran a RED light)' if not r["light_ok"]
+              else 'Traffic Light Respected : True')
+    print(f'===> Checks passed : {r["passed"]}')
+    return r["passed"]

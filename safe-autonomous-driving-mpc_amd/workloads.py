@@ -1,0 +1,84 @@
+"""Synthetic ego batches for the BASELINE.json configurations.
+
+Generator: numpy default_rng(seed) (PCG64).  Per ego (single-step microbench):
+  s0 ~ U(0, 0.8 s_max); d0 = d_ref(s0) + N(0, 0.05); o0 = o_ref(s0) + N(0, 0.01);
+  k0 = k_ref(s0); v0 = max(0.5, v_ref(s0) + N(0, 0.5)).
+Obstacle slabs:
+  'fsm2' / 'fsm3'  snapshot of an ObstaclesFSM (trajectory_tracking.py:292-327 presets): the dynamic
+                   car (v = 4 m/s) ahead of the ego w.p. 0.5 at s0 + U(8, 70); the RED light at tl_pos
+                   when 0 < tl_pos - s0 < tl_trigger_s.  max_obs = 2.
+  'const8'         8 constant-velocity cars: s_i = s0 + 25 + 50 i + U(0, 10), v_i ~ U(2, 10).
+"""
+import numpy as np
+
+from trajectory_loader import TrajectoryLoader, builtin_trajectory
+
+CONFIGS = {
+    # name: (trajectory, horizon N, batch B, seed, obstacle kind, GPUs in BASELINE.json)
+    "C1": dict(traj=1, N=10, B=1, seed=1, obstacles=None, gpus=0),
+    "C2": dict(traj=1, N=20, B=4096, seed=2, obstacles=None, gpus=1),
+    "C3": dict(traj=2, N=20, B=8192, seed=3, obstacles="fsm2", gpus=1),
+    "C4": dict(traj=3, N=30, B=16384, seed=4, obstacles="fsm3", gpus=4),
+    "C5": dict(traj=3, N=40, B=65536, seed=5, obstacles="const8", gpus=8),
+}
+
+_FSM = {"fsm2": dict(tl_pos=550.0, tl_trigger_s=100.0), "fsm3": dict(tl_pos=2000.0, tl_trigger_s=100.0)}
+
+_LOADERS = {}
+
+
+def loader(i):
+    if i not in _LOADERS:
+        _LOADERS[i] = TrajectoryLoader(builtin_trajectory(i))
+    return _LOADERS[i]
+
+
+def make_batch(name, B=None, seed=None, offset=0):
+    """Return dict(traj, N, x0 [B,5], obs [B,M,2] | None, n_obs [B] | None, max_obs).
+    `offset` skips the first `offset` egos of the same stream (for sharding across ranks)."""
+    cfg = CONFIGS[name]
+    B = cfg["B"] if B is None else int(B)
+    seed = cfg["seed"] if seed is None else seed
+    ld = loader(cfg["traj"])
+    rng = np.random.default_rng(seed)
+    tot = offset + B
+    s0 = rng.uniform(0.0, 0.8 * ld.s_max, tot)
+    nd = rng.normal(0, 0.05, tot)
+    no = rng.normal(0, 0.01, tot)
+    nv = rng.normal(0, 0.5, tot)
+    x0 = np.empty((B, 5))
+    for b in range(B):
+        i = offset + b
+        r = ld.get_state(s0[i])
+        x0[b] = (s0[i], r[1] + nd[i], r[2] + no[i], r[3], max(0.5, r[4] + nv[i]))
+    kind = cfg["obstacles"]
+    obs = n_obs = None
+    max_obs = 0
+    if kind in _FSM:
+        max_obs = 2
+        pc = rng.uniform(size=tot)
+        pd = rng.uniform(8.0, 70.0, tot)
+        obs = np.zeros((B, 2, 2))
+        n_obs = np.zeros(B, np.int32)
+        f = _FSM[kind]
+        for b in range(B):
+            i = offset + b
+            n = 0
+            if pc[i] < 0.5:
+                obs[b, n] = (x0[b, 0] + pd[i], 4.0)
+                n += 1
+            if 0.0 < f["tl_pos"] - x0[b, 0] < f["tl_trigger_s"]:
+                obs[b, n] = (f["tl_pos"], 0.0)
+                n += 1
+            n_obs[b] = n
+    elif kind == "const8":
+        max_obs = 8
+        u = rng.uniform(0, 10, (tot, 8))
+        v = rng.uniform(2, 10, (tot, 8))
+        obs = np.zeros((B, 8, 2))
+        for b in range(B):
+            i = offset + b
+            obs[b, :, 0] = x0[b, 0] + 25.0 + 50.0 * np.arange(8) + u[i]
+            obs[b, :, 1] = v[i]
+        n_obs = np.full(B, 8, np.int32)
+    return dict(traj=cfg["traj"], N=cfg["N"], x0=x0, obs=obs, n_obs=n_obs, max_obs=max_obs)
