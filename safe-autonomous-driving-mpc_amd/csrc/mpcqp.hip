@@ -125,56 +125,43 @@ __device__ void get_control(const DevTable& t, double s, double* out) {
 }
 
 // ------------------------------------------------------------------------------------------
-// per-instance LDS layout (doubles); stage arrays indexed k = 0..N, row arrays [j][k]
+// per-instance LDS layout (doubles); stage arrays indexed by stage k = 0..N
 // ------------------------------------------------------------------------------------------
 struct Lds {
     double* A5;    // [N][5]    a12,a14,a20,a23,a24 of A_k = I + J'_k  (a04 = dt)
-    double* Qs;    // [N+1][10] cost Hessian on (s,d,o,v), packed upper
-    double* qs;    // [N+1][4]
-    double* bs;    // [N+1][9]  soft row bounds
-    double* bb;    // [N][4]    box row bounds
-    double* rr;    // [N][2]    R * ubar
-    double* Qt;    // [N+1][10] Riccati stage Hessians (barrier / penalty augmented)
+    double* cst;   // [N+1][6]  cost data of stage k: (-d_ref', -o_ref', -v_ref') and the residuals r_d, r_o, r_v
+    double* Qt;    // [N+1][10] Riccati stage Hessians on (s,d,o,v) (barrier / penalty augmented), packed
     double* Rt;    // [N][2]
-    double* Kf;    // [N][10]   Riccati gains K_k (2x5)
-    double* Si;    // [N][3]    (1/l00, l10, 1/l11) of S_k = Ls Ls'
-    double* qh;    // [N+1][4]  LQR stage linear terms
-    double* gh;    // [N][2]
+    double* Kf;    // [N][10]   Riccati gains K_t (2x5)
+    double* Si;    // [N][3]    (1/l00, l10, 1/l11) of S_t = Ls Ls'
+    double* qh;    // [N+1][4]  LQR stage linear terms (state)
+    double* gh;    // [N][2]    LQR stage linear terms (control)
     double* kk;    // [N][2]
     double* Xr;    // [N+1][5]  rollout of the current iterate
     double* dX;    // [N+1][5]  rollout of the direction
     double* du;    // [N][2]    current iterate dU
     double* dud;   // [N][2]    direction dU
-    double* dub;   // [N][2]    backup (interior-point iterate during the polish)
-    double* ys;    // [N+1][4]  dual residual stage terms: cost part
-    double* ya;    // [N+1][4]  dual residual stage terms: multiplier part
-    double* zs;    // [N][2]
+    double* dub;   // [N][2]    interior-point iterate kept during the polish
+    double* yc;    // [N+1][4]  dual-residual stage terms: cost part
+    double* ya;    // [N+1][4]  dual-residual stage terms: multiplier part
+    double* zc;    // [N][2]
     double* za;    // [N][2]
     double* ub;    // [N][2]    linearisation point
     double* xb;    // [N+1][5]  nominal rollout / predict output
-    double* kap;   // [N+1]
-    // interior-point row state (soft rows [9][N+1], box rows [4][N])
-    double *rs, *rl, *rxi, *rnu, *pa4, *pa5, *tl;
-    double *bsv, *blv, *pab, *tlb;
-    double* cls;   // [9][N+1] polish row class, [4][N] box class after it
+    double* kap;   // [N+1]     k_ref(xbar_k); then shat_k (min obstacle prediction)
 };
 
 __host__ __device__ inline int lds_doubles(int N) {
     int NP = N + 1;
-    return N * 5 + NP * 10 + NP * 4 + NP * 9 + N * 4 + N * 2 + NP * 10 + N * 2 + N * 10 + N * 3 + NP * 4 + N * 2 +
-           N * 2 + NP * 5 + NP * 5 + N * 2 + N * 2 + N * 2 + NP * 4 + NP * 4 + N * 2 + N * 2 + N * 2 + NP * 5 + NP +
-           7 * 9 * NP + 4 * 4 * N + 9 * NP + 4 * N;
+    return N * 5 + NP * 6 + NP * 10 + N * 2 + N * 10 + N * 3 + NP * 4 + N * 2 + N * 2 + NP * 5 + NP * 5 + N * 2 +
+           N * 2 + N * 2 + NP * 4 + NP * 4 + N * 2 + N * 2 + N * 2 + NP * 5 + NP;
 }
 
 __device__ inline Lds carve(double* p, int N) {
     Lds L;
     int NP = N + 1;
     L.A5 = p; p += N * 5;
-    L.Qs = p; p += NP * 10;
-    L.qs = p; p += NP * 4;
-    L.bs = p; p += NP * 9;
-    L.bb = p; p += N * 4;
-    L.rr = p; p += N * 2;
+    L.cst = p; p += NP * 6;
     L.Qt = p; p += NP * 10;
     L.Rt = p; p += N * 2;
     L.Kf = p; p += N * 10;
@@ -187,37 +174,25 @@ __device__ inline Lds carve(double* p, int N) {
     L.du = p; p += N * 2;
     L.dud = p; p += N * 2;
     L.dub = p; p += N * 2;
-    L.ys = p; p += NP * 4;
+    L.yc = p; p += NP * 4;
     L.ya = p; p += NP * 4;
-    L.zs = p; p += N * 2;
+    L.zc = p; p += N * 2;
     L.za = p; p += N * 2;
     L.ub = p; p += N * 2;
     L.xb = p; p += NP * 5;
     L.kap = p; p += NP;
-    L.rs = p; p += 9 * NP;
-    L.rl = p; p += 9 * NP;
-    L.rxi = p; p += 9 * NP;
-    L.rnu = p; p += 9 * NP;
-    L.pa4 = p; p += 9 * NP;
-    L.pa5 = p; p += 9 * NP;
-    L.tl = p; p += 9 * NP;
-    L.bsv = p; p += 4 * N;
-    L.blv = p; p += 4 * N;
-    L.pab = p; p += 4 * N;
-    L.tlb = p; p += 4 * N;
-    L.cls = p; p += 9 * NP + 4 * N;
     return L;
 }
 
 // packed symmetric 4x4 on (s,d,o,v): index of (a,b)
-__device__ __forceinline__ int p4(int a, int b) {
+__host__ __device__ __forceinline__ int p4(int a, int b) {
     if (a > b) { int t = a; a = b; b = t; }
     return a == 0 ? b : (a == 1 ? 3 + b : (a == 2 ? 5 + b : 9));
 }
 // state index (0..4: s,d,o,k,v) of reduced index (0..3: s,d,o,v)
 __device__ __forceinline__ int st4(int a) { return a == 3 ? 4 : a; }
 
-// soft row coefficient vectors over (s,d,o,v) (oracle C[][] with the k entry dropped)
+// soft row coefficient vectors over (s,d,o,v) (the oracle's C[][] without the k entry)
 __device__ __forceinline__ void row_coef(int j, double h, double L, double T, double c[4]) {
     c[0] = c[1] = c[2] = c[3] = 0.0;
     switch (j) {
@@ -233,14 +208,47 @@ __device__ __forceinline__ void row_coef(int j, double h, double L, double T, do
     }
 }
 __device__ __forceinline__ double bsign(int j) { return (j & 1) ? -1.0 : 1.0; }   // box rows +u1,-u1,+u2,-u2
+__device__ __forceinline__ double dot4(const double c[4], const double x[4]) {
+    return fma(c[0], x[0], fma(c[1], x[1], fma(c[2], x[2], c[3] * x[3])));
+}
+// 1/x to full double precision: v_rcp_f64 + two Newton steps (no IEEE division sequence)
+__device__ __forceinline__ double frcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
+// ------------------------------------------------------------------------------------------
+// lane groups: IPW instances per 64-lane wavefront, GL = 64 / IPW lanes each
+// ------------------------------------------------------------------------------------------
+template <int GL>
+struct Grp {
+    int base;   // first lane of the group
+    __device__ __forceinline__ double sum(double v) const {
+#pragma unroll
+        for (int m = GL / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+        return v;
+    }
+    __device__ __forceinline__ double max(double v) const {
+#pragma unroll
+        for (int m = GL / 2; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, WAVE));
+        return v;
+    }
+    __device__ __forceinline__ double min(double v) const {
+#pragma unroll
+        for (int m = GL / 2; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, WAVE));
+        return v;
+    }
+    __device__ __forceinline__ double get(double v, int rel) const { return __shfl(v, base + rel, WAVE); }
+};
 
 // nonlinear rollout (predict, trajectory_tracking.py:87-114), bit-exact.  s, v, k do not depend on
 // the k_ref lookups, so they are rolled first; lane j then looks up k_ref(s_j); then d, o.
-__device__ void predict_wave(const DevTable& tab, const KParams& P, const double* x0, const double* uU,
-                             double* xout, double* kap, int lane) {
-    const int N = P.N;
-    const double dt = P.dt;
-    if (lane == 0) {
+__device__ void predict_grp(const DevTable& tab, int N, double dt, const double* x0, const double* uU, double* xout,
+                            double* kap, int ln) {
+    if (ln == 0) {
         double s = x0[0], k = x0[3], v = x0[4];
         for (int a = 0; a < 5; ++a) xout[a] = x0[a];
         for (int j = 0; j < N; ++j) {
@@ -254,13 +262,13 @@ __device__ void predict_wave(const DevTable& tab, const KParams& P, const double
         }
     }
     wave_sync();
-    if (lane < N) {
+    if (ln < N) {
         double st[5];
-        get_state(tab, xout[5 * lane], st, nullptr);
-        kap[lane] = st[3];
+        get_state(tab, xout[5 * ln], st, nullptr);
+        kap[ln] = st[3];
     }
     wave_sync();
-    if (lane == 0) {
+    if (ln == 0) {
         double d = x0[1], o = x0[2];
         for (int j = 0; j < N; ++j) {
             double v = xout[5 * j + 4], k = xout[5 * j + 3];
@@ -291,9 +299,9 @@ __device__ __forceinline__ void applyAT(const double* a, double dt, const double
     y[4] = fma(dt, m[0], fma(a[1], m[1], fma(a[4], m[2], m[4])));
 }
 
-// X = G u : rollout of the linear model from x_0 = 0 (uniform; lane 0 writes)
-__device__ void rollout_lin(const Lds& S, int N, double dt, const double* u, double* X, int lane) {
-    if (lane == 0) {
+// X = G u : rollout of the linear model from x_0 = 0 (group-uniform; lane 0 of the group writes)
+__device__ void rollout_lin(const Lds& S, int N, double dt, const double* u, double* X, int ln) {
+    if (ln == 0) {
         double x[5] = {0, 0, 0, 0, 0};
         for (int a = 0; a < 5; ++a) X[a] = 0.0;
         for (int j = 0; j < N; ++j) {
@@ -307,83 +315,69 @@ __device__ void rollout_lin(const Lds& S, int N, double dt, const double* u, dou
     wave_sync();
 }
 
-// Riccati factorisation of  min sum 0.5 x'Qt x + 0.5 u'Rt u,  x_{k+1} = A_k x_k + B u_k,  x_0 = 0.
-// S_k = Rt_k + B'P B = Ls Ls' (2x2 Cholesky), W = Ls^-1 B'P A, K = -Ls^-T W, P <- Qt + A'PA - W'W.
-// The Cholesky form keeps ~2 more digits than an explicit S^-1 when the barrier weights reach
-// 1e12+.  Wave-uniform; lane 0 writes Kf, Si.
-__device__ void riccati_factor(const Lds& S, int N, double dt, int lane) {
-    double Pm[5][5];
-#pragma unroll
-    for (int a = 0; a < 5; ++a)
-#pragma unroll
-        for (int c = 0; c < 5; ++c) Pm[a][c] = 0.0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) Pm[st4(a)][st4(c)] = S.Qt[10 * N + p4(a, c)];
+// Riccati factorisation of  min sum 0.5 x'Qt x + 0.5 u'Rt u,  x_{t+1} = A_t x_t + B u_t,  x_0 = 0,
+// spread over 25 lanes of the group: lane (i, j) = ln / 5, ln % 5 holds P[i][j].  Per stage:
+// M = P A (gather row i of P), S = Rt + B'P B = Ls Ls' (uniform), W = Ls^-1 B'M, K = -Ls^-T W,
+// P <- Qt + A'M - W'W (gather column j of M), symmetrised.  The Cholesky form keeps ~2 more digits
+// than an explicit S^-1 once barrier weights reach 1e12.
+template <int GL>
+__device__ void riccati_factor(const Lds& S, const Grp<GL>& G, int N, double dt, int ln) {
+    const int i = ln / 5, j = ln - 5 * (ln / 5);
+    const bool act = ln < 25;
+    const int ri = i == 4 ? 3 : i, rj = j == 4 ? 3 : j;
+    const bool qv = act && i != 3 && j != 3;
+    const int qo = qv ? p4(ri, rj) : 0;
+    double P = qv ? S.Qt[10 * N + qo] : 0.0;
     const double dt2 = dt * dt;
     for (int t = N - 1; t >= 0; --t) {
         const double* a = S.A5 + 5 * t;
         const double a12 = a[0], a14 = a[1], a20 = a[2], a23 = a[3], a24 = a[4];
-        double M[5][5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            M[i][0] = fma(Pm[i][2], a20, Pm[i][0]);
-            M[i][1] = Pm[i][1];
-            M[i][2] = fma(Pm[i][1], a12, Pm[i][2]);
-            M[i][3] = fma(Pm[i][2], a23, Pm[i][3]);
-            M[i][4] = fma(Pm[i][0], dt, fma(Pm[i][1], a14, fma(Pm[i][2], a24, Pm[i][4])));
-        }
-        double s00 = fma(dt2, Pm[3][3], S.Rt[2 * t]);
-        double s01 = dt2 * Pm[3][4];
-        double s11 = fma(dt2, Pm[4][4], S.Rt[2 * t + 1]);
+        const double r0 = S.Rt[2 * t], r1 = S.Rt[2 * t + 1];
+        const double qt = (qv && t >= 1) ? S.Qt[10 * t + qo] : 0.0;
+        // M[i][j] = P[i][j] + sum_l P[i][l] J'[l][j]
+        const double p0 = G.get(P, 5 * i + 0), p1 = G.get(P, 5 * i + 1), p2 = G.get(P, 5 * i + 2);
+        double M = P;
+        if (j == 0) M = fma(p2, a20, M);
+        else if (j == 2) M = fma(p1, a12, M);
+        else if (j == 3) M = fma(p2, a23, M);
+        else if (j == 4) M = fma(p0, dt, fma(p1, a14, fma(p2, a24, M)));
+        // S = Rt + dt^2 P[{3,4},{3,4}]  (uniform)
+        const double P33 = G.get(P, 18), P34 = G.get(P, 19), P44 = G.get(P, 24);
+        double s00 = fma(dt2, P33, r0), s01 = dt2 * P34, s11 = fma(dt2, P44, r1);
         if (!(s00 > 0.0)) s00 = 1e-300 + fabs(s00);
-        double l00 = sqrt(s00), l10 = s01 / l00, r11 = s11 - l10 * l10;
+        const double l00 = sqrt(s00), il00 = frcp(l00), l10 = s01 * il00;
+        double r11 = s11 - l10 * l10;
         if (!(r11 > 1e-14 * s11)) r11 = 1e-14 * fabs(s11) + 1e-300;
-        double l11 = sqrt(r11);
-        double il00 = 1.0 / l00, il11 = 1.0 / l11;
-        double W0[5], W1[5], K0[5], K1[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            W0[j] = dt * M[3][j] * il00;
-            W1[j] = (dt * M[4][j] - l10 * W0[j]) * il11;
-            K1[j] = -W1[j] * il11;
-            K0[j] = -(W0[j] + l10 * K1[j]) * il00;
+        const double l11 = sqrt(r11), il11 = frcp(l11);
+        // column j of M, and M[3][i], M[4][i]
+        const double m0 = G.get(M, j), m1 = G.get(M, 5 + j), m2 = G.get(M, 10 + j);
+        const double m3 = G.get(M, 15 + j), m4 = G.get(M, 20 + j);
+        const double mi3 = G.get(M, 15 + i), mi4 = G.get(M, 20 + i);
+        const double W0j = dt * m3 * il00, W1j = (dt * m4 - l10 * W0j) * il11;
+        const double W0i = dt * mi3 * il00, W1i = (dt * mi4 - l10 * W0i) * il11;
+        if (act && i == 0) {
+            const double K1 = -W1j * il11;
+            const double K0 = -(W0j + l10 * K1) * il00;
+            S.Kf[10 * t + j] = K0;
+            S.Kf[10 * t + 5 + j] = K1;
         }
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < 5; ++j) { S.Kf[10 * t + j] = K0[j]; S.Kf[10 * t + 5 + j] = K1[j]; }
-            S.Si[3 * t] = il00; S.Si[3 * t + 1] = l10; S.Si[3 * t + 2] = il11;
-        }
-        if (t >= 1) {
-            double Pn[5][5];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                Pn[0][j] = fma(a20, M[2][j], M[0][j]);
-                Pn[1][j] = M[1][j];
-                Pn[2][j] = fma(a12, M[1][j], M[2][j]);
-                Pn[3][j] = fma(a23, M[2][j], M[3][j]);
-                Pn[4][j] = fma(dt, M[0][j], fma(a14, M[1][j], fma(a24, M[2][j], M[4][j])));
-            }
-            const double* qt = S.Qt + 10 * t;
-#pragma unroll
-            for (int i = 0; i < 5; ++i)
-#pragma unroll
-                for (int j = i; j < 5; ++j) {
-                    double ww = fma(W0[i], W0[j], W1[i] * W1[j]);
-                    double q = (i != 3 && j != 3) ? qt[p4(i == 4 ? 3 : i, j == 4 ? 3 : j)] : 0.0;
-                    double val = 0.5 * ((Pn[i][j] - ww) + (Pn[j][i] - ww)) + q;
-                    Pm[i][j] = val;
-                    Pm[j][i] = val;
-                }
-        }
+        if (ln == 0) { S.Si[3 * t] = il00; S.Si[3 * t + 1] = l10; S.Si[3 * t + 2] = il11; }
+        // (A'M)[i][j] = M[i][j] + sum_l J'[l][i] M[l][j]
+        double Nij = M;
+        if (i == 0) Nij = fma(a20, m2, Nij);
+        else if (i == 2) Nij = fma(a12, m1, Nij);
+        else if (i == 3) Nij = fma(a23, m2, Nij);
+        else if (i == 4) Nij = fma(dt, m0, fma(a14, m1, fma(a24, m2, Nij)));
+        const double Pn = Nij - fma(W0i, W0j, W1i * W1j);
+        const double Pt = G.get(Pn, 5 * j + i);
+        P = act ? 0.5 * (Pn + Pt) + qt : 0.0;
     }
     wave_sync();
 }
 
 // LQR solve with the factorisation: linear terms -qh (stages 1..N), -gh (controls).
-// Writes dud (controls) and dX (states, x_0 = 0).  Wave-uniform; lane 0 writes.
-__device__ void riccati_solve(const Lds& S, int N, double dt, int lane) {
+// Writes dud (controls) and dX (states, x_0 = 0).  Group-uniform; lane 0 of the group writes.
+__device__ void riccati_solve(const Lds& S, int N, double dt, int ln) {
     double p5[5] = {0, 0, 0, 0, 0};
 #pragma unroll
     for (int a = 0; a < 4; ++a) p5[st4(a)] = S.qh[4 * N + a];
@@ -395,7 +389,7 @@ __device__ void riccati_solve(const Lds& S, int N, double dt, int lane) {
         double w1 = (h1 - si[1] * w0) * si[2];
         double k1 = w1 * si[2];
         double k0 = (w0 - si[1] * k1) * si[0];
-        if (lane == 0) { S.kk[2 * t] = k0; S.kk[2 * t + 1] = k1; }
+        if (ln == 0) { S.kk[2 * t] = k0; S.kk[2 * t + 1] = k1; }
         if (t >= 1) {
             double pa[5];
             applyAT(S.A5 + 5 * t, dt, p5, pa);
@@ -407,7 +401,7 @@ __device__ void riccati_solve(const Lds& S, int N, double dt, int lane) {
         }
     }
     wave_sync();
-    if (lane == 0) {
+    if (ln == 0) {
         double x[5] = {0, 0, 0, 0, 0};
         for (int a = 0; a < 5; ++a) S.dX[a] = 0.0;
         for (int t = 0; t < N; ++t) {
@@ -428,8 +422,7 @@ __device__ void riccati_solve(const Lds& S, int N, double dt, int lane) {
     wave_sync();
 }
 
-// max |g_d| and the scale max(|g_cost|, |g_mult|) of the dual residual g = G'(y) + z, by the
-// adjoint recursion over the stage terms ys (cost) and ya (multipliers).  Wave-uniform.
+// max |g| and the scale max(|g_cost|, |g_mult|) of the dual residual g = G'y + z (adjoint recursion)
 __device__ void dual_norms(const Lds& S, int N, double dt, double& rdmax, double& sd) {
     double mc[5] = {0, 0, 0, 0, 0}, ma[5] = {0, 0, 0, 0, 0};
     rdmax = 0.0;
@@ -437,11 +430,11 @@ __device__ void dual_norms(const Lds& S, int N, double dt, double& rdmax, double
     for (int k = N; k >= 1; --k) {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-            mc[st4(a)] += S.ys[4 * k + a];
+            mc[st4(a)] += S.yc[4 * k + a];
             ma[st4(a)] += S.ya[4 * k + a];
         }
         const int t = k - 1;
-        double gc0 = fma(dt, mc[3], S.zs[2 * t]), gc1 = fma(dt, mc[4], S.zs[2 * t + 1]);
+        double gc0 = fma(dt, mc[3], S.zc[2 * t]), gc1 = fma(dt, mc[4], S.zc[2 * t + 1]);
         double ga0 = fma(dt, ma[3], S.za[2 * t]), ga1 = fma(dt, ma[4], S.za[2 * t + 1]);
         rdmax = fmax(rdmax, fmax(fabs(gc0 + ga0), fabs(gc1 + ga1)));
         sd = fmax(sd, fmax(fmax(fabs(gc0), fabs(gc1)), fmax(fabs(ga0), fabs(ga1))));
@@ -455,58 +448,123 @@ __device__ void dual_norms(const Lds& S, int N, double dt, double& rdmax, double
     }
 }
 
+// cost Hessian (packed 4x4 on s,d,o,v) and gradient of stage k from cst = (-d', -o', -v', r_d, r_o, r_v):
+// Q = 2 sum_j w_j m_j m_j',  q = 2 sum_j w_j r_j m_j,  m_j = e_j + (-ref_j') e_s   
+__device__ __forceinline__ void stage_cost(const double* cst, double wd, double wo, double wv, double Q[10],
+                                           double q[4]) {
+    const double w[3] = {2.0 * wd, 2.0 * wo, 2.0 * wv};
+#pragma unroll
+    for (int a = 0; a < 10; ++a) Q[a] = 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) q[a] = 0.0;
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+        const double m0 = cst[jj];        // s entry; the own entry (index jj+1) is 1
+        const double r = cst[3 + jj];
+        Q[p4(0, 0)] = fma(w[jj] * m0, m0, Q[p4(0, 0)]);
+        Q[p4(0, jj + 1)] += w[jj] * m0;
+        Q[p4(jj + 1, jj + 1)] += w[jj];
+        q[0] = fma(w[jj] * r, m0, q[0]);
+        q[jj + 1] += w[jj] * r;
+    }
+}
+
 #define POLISH_DELTA 1e-11
 #define POLISH_REFINE 4
 #define POLISH_ROUNDS 6
+#define MU0 1.0
+
+// Row slots: the 9 soft rows and 4 box rows of a stage are spread over P lanes (part = lane % P):
+// lane slot s holds soft row j = part * R + s (if < 9) and box row part * RB + s (if < 4).
+template <int P>
+struct Parts {
+    static constexpr int R = (NROW + P - 1) / P;
+    static constexpr int RB = (NBOX + P - 1) / P;
+};
 
 // ------------------------------------------------------------------------------------------
-// the solver kernel: one wavefront per MPC instance
+// the solver kernel: one wavefront per MPC instance; stage k = 1..N is owned by the P lanes
+// (k-1)*P .. (k-1)*P+P-1 (control t = k-1 with it); 25 lanes run the Riccati factorisation;
+// the vector recursions run wave-uniformly from LDS.
 // ------------------------------------------------------------------------------------------
+template <int P>
 __global__ void __launch_bounds__(WAVE)
-mpc_solve_kernel(DevTable tab, KParams P, int B, const double* __restrict__ x0g, const double* __restrict__ obsg,
+mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g, const double* __restrict__ obsg,
                  const int* __restrict__ nobsg, const double* __restrict__ ubarg, double* __restrict__ u0g,
                  double* __restrict__ Ug, double* __restrict__ Xg, int* __restrict__ statusg,
                  int* __restrict__ itersg) {
+    constexpr int R = Parts<P>::R, RB = Parts<P>::RB;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int b = blockIdx.x;
     if (b >= B) return;
-    const int lane = threadIdx.x;
-    const int N = P.N;
+    const int ln = threadIdx.x;
+    const Grp<WAVE> G{0};
+    const int N = Pr.N;
     const int NP = N + 1;
-    const double dt = P.dt;
-    const double rho = P.rho;
-    const double hL = P.L / 2.0;
+    const double dt = Pr.dt;
+    const double rho = Pr.rho;
+    const double hL = Pr.L / 2.0;
     Lds S = carve(smem, N);
 
     double x0[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) x0[j] = x0g[5 * (size_t)b + j];
     int nobs = nobsg ? nobsg[b] : 0;
-    nobs = nobs < 0 ? 0 : (nobs > P.max_obs ? P.max_obs : nobs);
-    const double* obs = obsg ? obsg + (size_t)b * P.max_obs * 2 : nullptr;
+    nobs = nobs < 0 ? 0 : (nobs > Pr.max_obs ? Pr.max_obs : nobs);
+    const double* obs = obsg ? obsg + (size_t)b * Pr.max_obs * 2 : nullptr;
     const bool has_obs = nobs > 0;
-    const bool live = lane < N;     // lane owns soft rows of stage k = lane+1 and box rows of control t = lane
-    const int k = lane + 1;
+
+    // stage ownership
+    const int part = ln % P;
+    const int k = ln / P + 1;                 // stage of this lane
+    const bool live = k <= N;                 // lane owns rows of stage k (and boxes of control k-1)
+    const int sbase = ln - part;              // first lane of this stage
+    const bool lead = live && part == 0;      // writes the stage sums
+
+    // row slots of this lane
+    int rj[R];
+    bool ron[R];
+    double cf[R][4];
+#pragma unroll
+    for (int s = 0; s < R; ++s) {
+        rj[s] = part * R + s;
+        ron[s] = live && rj[s] < NROW && ((rj[s] != 6 && rj[s] != 7) || has_obs);
+        row_coef(rj[s] < NROW ? rj[s] : 0, hL, Pr.L, Pr.tgap, cf[s]);
+    }
+    int bj[RB];
+    bool bon[RB];
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+        bj[s] = part * RB + s;
+        bon[s] = live && bj[s] < NBOX;
+    }
+    // sum of a per-lane partial over the P lanes of the stage (valid on the stage's part-0 lane)
+    auto stage_sum = [&](double v) {
+        double r = v;
+#pragma unroll
+        for (int q = 1; q < P; ++q) r += G.get(v, sbase + q);
+        return r;
+    };
 
     // ---- K1: linearisation point ---------------------------------------------------------
-    if (live) {
+    if (ln < N) {
         if (ubarg) {
-            S.ub[2 * lane] = ubarg[(size_t)b * 2 * N + 2 * lane];
-            S.ub[2 * lane + 1] = ubarg[(size_t)b * 2 * N + 2 * lane + 1];
+            S.ub[2 * ln] = ubarg[(size_t)b * 2 * N + 2 * ln];
+            S.ub[2 * ln + 1] = ubarg[(size_t)b * 2 * N + 2 * ln + 1];
         } else {
             // warm start, trajectory_tracking.py:224-246: s_curr advanced by repeated addition,
-            // sticky brake flag over steps 0..lane
+            // sticky brake flag over steps 0..ln
             double s_curr = x0[0], v_curr = x0[4];
             bool brake = false;
-            for (int j = 0; j <= lane; ++j) {
+            for (int j = 0; j <= ln; ++j) {
                 if (j > 0) s_curr += v_curr * dt;
                 for (int i = 0; i < nobs; ++i)
-                    if ((obs[2 * i] - s_curr) < P.brake_distance) brake = true;
+                    if ((obs[2 * i] - s_curr) < Pr.brake_distance) brake = true;
             }
             double ur[2];
             get_control(tab, s_curr, ur);
-            S.ub[2 * lane] = ur[0];
-            S.ub[2 * lane + 1] = brake ? P.brake_accel : ur[1];
+            S.ub[2 * ln] = ur[0];
+            S.ub[2 * ln + 1] = brake ? Pr.brake_accel : ur[1];
         }
     }
     wave_sync();
@@ -514,660 +572,560 @@ mpc_solve_kernel(DevTable tab, KParams P, int B, const double* __restrict__ x0g,
     int nsoft = 0;
     for (int j = 0; j < NROW; ++j) nsoft += ((j != 6 && j != 7) || has_obs) ? 1 : 0;
     const double Mtot = (double)(2 * nsoft * N + NBOX * N);
-    const double R0 = 2.0 * P.w_u1, R1 = 2.0 * P.w_u2;
+    const double R0 = 2.0 * Pr.w_u1, R1 = 2.0 * Pr.w_u2;
 
-    const int nsqp = P.sqp_iters < 0 ? 0 : P.sqp_iters;   // 0: return ubar and predict(x0, ubar)
+    const int nsqp = Pr.sqp_iters < 0 ? 0 : Pr.sqp_iters;   // 0: return ubar and predict(x0, ubar)
     int status = MPC_OK, total_it = 0;
     for (int sqp = 0; sqp < nsqp; ++sqp) {
-        // ---- K1: nominal rollout == predict(x0, ubar) ------------------------------------
-        predict_wave(tab, P, x0, S.ub, S.xb, S.kap, lane);
+        // ---- K1: nominal rollout == predict(x0, ubar), into Xr ------------------------------
+        predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, ln);
         // ---- K2: stage data of QP(ubar) ----------------------------------------------------
-        const bool gn = P.linearization != 0;
+        const bool gn = Pr.linearization != 0;
         double refk[5], slk[4];
-        if (lane <= N) get_state(tab, S.xb[5 * lane], refk, slk);
-        if (live) {
-            const double* x = S.xb + 5 * lane;
+        if (ln <= N) get_state(tab, S.Xr[5 * ln], refk, slk);
+        if (ln < N) {
+            const double* x = S.Xr + 5 * ln;
             double dk = gn ? slk[2] : 0.0;
-            S.A5[5 * lane + 0] = dt * x[4];
-            S.A5[5 * lane + 1] = dt * x[2];
-            S.A5[5 * lane + 2] = dt * (-x[4] * dk);
-            S.A5[5 * lane + 3] = dt * x[4];
-            S.A5[5 * lane + 4] = dt * (x[3] - refk[3]);
+            S.A5[5 * ln + 0] = dt * x[4];
+            S.A5[5 * ln + 1] = dt * x[2];
+            S.A5[5 * ln + 2] = dt * (-x[4] * dk);
+            S.A5[5 * ln + 3] = dt * x[4];
+            S.A5[5 * ln + 4] = dt * (x[3] - refk[3]);
         }
-        double bscale_l = 0.0;
-        if (lane >= 1 && lane <= N) {
-            const int kk = lane;
-            const double* x = S.xb + 5 * kk;
-            double ref[3] = {refk[1], refk[2], refk[4]};
-            double dref[3] = {gn ? slk[0] : 0.0, gn ? slk[1] : 0.0, gn ? slk[3] : 0.0};
-            double w[3] = {P.w_d, P.w_o, P.w_v};
-            int idx[3] = {1, 2, 4};
-            double Qp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                double m[4] = {-dref[j], 0.0, 0.0, 0.0};
-                m[j + 1] = 1.0;
-                double r0 = x[idx[j]] - ref[j];
-#pragma unroll
-                for (int a = 0; a < 4; ++a) {
-                    q4[a] += 2.0 * w[j] * r0 * m[a];
-#pragma unroll
-                    for (int c = a; c < 4; ++c) Qp[p4(a, c)] += 2.0 * w[j] * m[a] * m[c];
-                }
+        // cost data of stage k (lookups done by lane k)
+        {
+            const double rk1 = G.get(refk[1], k), rk2 = G.get(refk[2], k), rk4 = G.get(refk[4], k);
+            const double sk0 = G.get(slk[0], k), sk1 = G.get(slk[1], k), sk3 = G.get(slk[3], k);
+            if (lead) {
+                const double* x = S.Xr + 5 * k;
+                S.cst[6 * k + 0] = gn ? -sk0 : 0.0;
+                S.cst[6 * k + 1] = gn ? -sk1 : 0.0;
+                S.cst[6 * k + 2] = gn ? -sk3 : 0.0;
+                S.cst[6 * k + 3] = x[1] - rk1;
+                S.cst[6 * k + 4] = x[2] - rk2;
+                S.cst[6 * k + 5] = x[4] - rk4;
             }
-            for (int a = 0; a < 10; ++a) S.Qs[10 * kk + a] = Qp[a];
-            for (int a = 0; a < 4; ++a) S.qs[4 * kk + a] = q4[a];
-            const double Lw = P.L, sl = P.sl;
-            double pv0 = x[1], pv1 = x[1] + hL * x[2], pv2 = x[1] + Lw * x[2];
-            double bk[NROW];
-            bk[0] = -sl - pv0; bk[1] = -(sl - pv0);
-            bk[2] = -sl - pv1; bk[3] = -(sl - pv1);
-            bk[4] = -sl - pv2; bk[5] = -(sl - pv2);
-            bk[6] = 0.0; bk[7] = 0.0;
-            if (has_obs) {
-                double shat = INFINITY;
+        }
+        // row bounds of this lane's rows, box bounds of its boxes
+        double bk[R], bb[RB];
+        double bscale_l = 0.0;
+        {
+            double shat = INFINITY;
+            if (live && has_obs)
                 for (int i = 0; i < nobs; ++i) {
-                    double sp = obs[2 * i] + obs[2 * i + 1] * (kk * dt);
+                    double sp = obs[2 * i] + obs[2 * i + 1] * (k * dt);
                     shat = sp < shat ? sp : shat;
                 }
-                bk[6] = -(shat - P.osd - x[0]);
-                bk[7] = -(shat - x[0] - P.tgap * x[4]);
-            }
-            bk[8] = -x[4];
+            const double* x = S.Xr + 5 * (live ? k : 0);
+            const double sl = Pr.sl;
+            const double pv0 = x[1], pv1 = x[1] + hL * x[2], pv2 = x[1] + Pr.L * x[2];
 #pragma unroll
-            for (int j = 0; j < NROW; ++j) {
-                S.bs[NROW * kk + j] = bk[j];
-                if ((j != 6 && j != 7) || has_obs) bscale_l = fmax(bscale_l, fabs(bk[j]));
+            for (int s = 0; s < R; ++s) {
+                const int j = rj[s];
+                double v = 0.0;
+                switch (j) {
+                    case 0: v = -sl - pv0; break;
+                    case 1: v = -(sl - pv0); break;
+                    case 2: v = -sl - pv1; break;
+                    case 3: v = -(sl - pv1); break;
+                    case 4: v = -sl - pv2; break;
+                    case 5: v = -(sl - pv2); break;
+                    case 6: v = has_obs ? -(shat - Pr.osd - x[0]) : 0.0; break;
+                    case 7: v = has_obs ? -(shat - x[0] - Pr.tgap * x[4]) : 0.0; break;
+                    case 8: v = -x[4]; break;
+                    default: v = 0.0; break;
+                }
+                bk[s] = ron[s] ? v : 0.0;
+                bscale_l = fmax(bscale_l, fabs(bk[s]));
+            }
+            const double ub0 = live ? S.ub[2 * (k - 1)] : 0.0, ub1 = live ? S.ub[2 * (k - 1) + 1] : 0.0;
+#pragma unroll
+            for (int s = 0; s < RB; ++s) {
+                double v = 0.0;
+                switch (bj[s]) {
+                    case 0: v = Pr.u_min0 - ub0; break;
+                    case 1: v = -(Pr.u_max0 - ub0); break;
+                    case 2: v = Pr.u_min1 - ub1; break;
+                    case 3: v = -(Pr.u_max1 - ub1); break;
+                    default: v = 0.0; break;
+                }
+                bb[s] = bon[s] ? v : 0.0;
+                bscale_l = fmax(bscale_l, fabs(bb[s]));
             }
         }
-        if (live) {
-            double ub0 = S.ub[2 * lane], ub1 = S.ub[2 * lane + 1];
-            S.bb[4 * lane + 0] = P.u_min0 - ub0;
-            S.bb[4 * lane + 1] = -(P.u_max0 - ub0);
-            S.bb[4 * lane + 2] = P.u_min1 - ub1;
-            S.bb[4 * lane + 3] = -(P.u_max1 - ub1);
-            S.rr[2 * lane] = R0 * ub0;
-            S.rr[2 * lane + 1] = R1 * ub1;
-#pragma unroll
-            for (int j = 0; j < NBOX; ++j) bscale_l = fmax(bscale_l, fabs(S.bb[4 * lane + j]));
-        }
-        const double bscale = wave_max(bscale_l);
+        const double bscale = G.max(bscale_l);
         wave_sync();
 
-        // ---- K4: PDIP ------------------------------------------------------------------------
-        if (live) {
+        // ---- K4: PDIP; interior-point state of this lane's rows in registers ---------------------
+        double rs[R], rl[R], rxi[R], rnu[R], sb[RB], lb[RB];
 #pragma unroll
-            for (int j = 0; j < NROW; ++j) {
-                const bool on = (j != 6 && j != 7) || has_obs;
-                double r0 = -S.bs[NROW * k + j];
-                double xi = (r0 < 0 ? -r0 : 0.0) + XI0;
-                S.rxi[j * NP + k] = on ? xi : 1.0;
-                S.rs[j * NP + k] = on ? r0 + xi : 1.0;
-                S.rl[j * NP + k] = on ? 1.0 : 0.0;
-                S.rnu[j * NP + k] = on ? rho - 1.0 : 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < NBOX; ++j) {
-                double r0 = -S.bb[4 * lane + j];
-                S.bsv[j * N + lane] = r0 > 1.0 ? r0 : 1.0;
-                S.blv[j * N + lane] = 1.0;
-            }
-            S.du[2 * lane] = 0.0;
-            S.du[2 * lane + 1] = 0.0;
+        for (int s = 0; s < R; ++s) {
+            // centred start: xi covers the violation, s*lam = MU0 with lam <= rho/2, nu = rho - lam
+            const double r0 = -bk[s];
+            const double xi = (r0 < 0 ? -r0 : 0.0) + XI0;
+            const double sv = r0 + xi;
+            const double lam = fmin(MU0 * frcp(sv), 0.5 * rho);
+            rxi[s] = xi; rs[s] = sv; rl[s] = lam; rnu[s] = rho - lam;
         }
+#pragma unroll
+        for (int s = 0; s < RB; ++s) {
+            const double r0 = -bb[s];
+            sb[s] = r0 > 1.0 ? r0 : 1.0;
+            lb[s] = 1.0;
+        }
+        if (ln < N) { S.du[2 * ln] = 0.0; S.du[2 * ln + 1] = 0.0; }
         wave_sync();
 
-        int it;
-        int st_here = MPC_MAX_ITER;
-        int stall = 0;
-        bool have_acc = false, inf_acc = false;
-        double acc0 = 0.0, acc1 = 0.0, mu = 0.0;
-        for (it = 0; it < P.max_iter; ++it) {
-            rollout_lin(S, N, dt, S.du, S.Xr, lane);
-            // -- stage-parallel residuals -------------------------------------------------------
+        int it = 0, st_here = MPC_MAX_ITER, stall = 0;
+        bool done = false;
+        double mu = 0.0;
+        for (int iter = 0; iter < Pr.max_iter; ++iter) {
+            rollout_lin(S, N, dt, S.du, S.dX, ln);
+            // -- stage-parallel residuals ------------------------------------------------------
+            double x4[4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) x4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
+            const double du0 = live ? S.du[2 * (k - 1)] : 0.0, du1 = live ? S.du[2 * (k - 1) + 1] : 0.0;
             double rpmax = 0.0, rxmax = 0.0, comp = 0.0;
-            if (live) {
-                double x4[4];
+            double ya[4] = {0, 0, 0, 0}, za0 = 0.0, za1 = 0.0;
 #pragma unroll
-                for (int a = 0; a < 4; ++a) x4[a] = S.Xr[5 * k + st4(a)];
-                double yc[4], ya[4] = {0, 0, 0, 0};
+            for (int s = 0; s < R; ++s) {
+                if (!ron[s]) continue;
+                const double rp = dot4(cf[s], x4) + rxi[s] - rs[s] - bk[s];
+                const double rx = rho - rl[s] - rnu[s];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) ya[a] = fma(-rl[s], cf[s][a], ya[a]);
+                rpmax = fmax(rpmax, fabs(rp));
+                rxmax = fmax(rxmax, fabs(rx));
+                comp = fma(rs[s], rl[s], fma(rxi[s], rnu[s], comp));
+            }
+#pragma unroll
+            for (int s = 0; s < RB; ++s) {
+                if (!bon[s]) continue;
+                const double rp = bsign(bj[s]) * ((bj[s] < 2) ? du0 : du1) - sb[s] - bb[s];
+                rpmax = fmax(rpmax, fabs(rp));
+                comp = fma(sb[s], lb[s], comp);
+                if (bj[s] < 2) za0 += -bsign(bj[s]) * lb[s]; else za1 += -bsign(bj[s]) * lb[s];
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a) ya[a] = stage_sum(ya[a]);
+            za0 = stage_sum(za0);
+            za1 = stage_sum(za1);
+            if (lead) {
+                double Qs[10], qs[4], yc[4];
+                stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
-                    double acc = S.qs[4 * k + a];
+                    double acc = qs[a];
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) acc = fma(S.Qs[10 * k + p4(a, c)], x4[c], acc);
+                    for (int c = 0; c < 4; ++c) acc = fma(Qs[p4(a, c)], x4[c], acc);
                     yc[a] = acc;
                 }
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) {
-                    if ((j == 6 || j == 7) && !has_obs) continue;
-                    double c[4];
-                    row_coef(j, hL, P.L, P.tgap, c);
-                    const double sv = S.rs[j * NP + k], lv = S.rl[j * NP + k];
-                    const double xv = S.rxi[j * NP + k], nv = S.rnu[j * NP + k];
-                    double cx = c[0] * x4[0] + c[1] * x4[1] + c[2] * x4[2] + c[3] * x4[3];
-                    double r = cx + xv - sv - S.bs[NROW * k + j];
-                    double rx = rho - lv - nv;
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) ya[a] = fma(-lv, c[a], ya[a]);
-                    rpmax = fmax(rpmax, fabs(r));
-                    rxmax = fmax(rxmax, fabs(rx));
-                    comp += sv * lv + xv * nv;
-                }
-#pragma unroll
-                for (int a = 0; a < 4; ++a) { S.ys[4 * k + a] = yc[a]; S.ya[4 * k + a] = ya[a]; }
-                const double du0 = S.du[2 * lane], du1 = S.du[2 * lane + 1];
-                S.zs[2 * lane] = fma(R0, du0, S.rr[2 * lane]);
-                S.zs[2 * lane + 1] = fma(R1, du1, S.rr[2 * lane + 1]);
-                S.za[2 * lane] = -S.blv[0 * N + lane] + S.blv[1 * N + lane];
-                S.za[2 * lane + 1] = -S.blv[2 * N + lane] + S.blv[3 * N + lane];
-#pragma unroll
-                for (int j = 0; j < NBOX; ++j) {
-                    double uu = (j < 2) ? du0 : du1;
-                    double r = bsign(j) * uu - S.bsv[j * N + lane] - S.bb[4 * lane + j];
-                    rpmax = fmax(rpmax, fabs(r));
-                    comp += S.bsv[j * N + lane] * S.blv[j * N + lane];
-                }
+                for (int a = 0; a < 4; ++a) { S.yc[4 * k + a] = yc[a]; S.ya[4 * k + a] = ya[a]; }
+                S.zc[2 * (k - 1)] = fma(R0, du0, R0 * S.ub[2 * (k - 1)]);
+                S.zc[2 * (k - 1) + 1] = fma(R1, du1, R1 * S.ub[2 * (k - 1) + 1]);
+                S.za[2 * (k - 1)] = za0;
+                S.za[2 * (k - 1) + 1] = za1;
             }
-            rpmax = wave_max(rpmax);
-            rxmax = wave_max(rxmax);
-            comp = wave_sum(comp);
+            rpmax = G.max(rpmax);
+            rxmax = G.max(rxmax);
+            comp = G.sum(comp);
             wave_sync();
             double rdmax, sd;
             dual_norms(S, N, dt, rdmax, sd);
             mu = comp / Mtot;
-            if (!(mu == mu) || !(rdmax == rdmax)) { st_here = MPC_NUMERICAL; break; }
-            // the dual residual carries the O(eps/mu) noise of the active multipliers: tolerance 1e3*tol
-            if (rdmax <= 1e3 * P.tol * (1.0 + sd) && rpmax <= P.tol * (1.0 + bscale) && rxmax <= P.tol * rho &&
-                mu <= P.tol_mu) {
-                st_here = MPC_OK;
+            if (!(mu == mu) || !(rdmax == rdmax)) { st_here = MPC_NUMERICAL; it = iter; done = true; break; }
+            if (mu <= Pr.tol_mu && rpmax <= 10.0 * Pr.tol * (1.0 + bscale) && rxmax <= Pr.tol * rho) {
+                // converged: the polish then makes the active set exact;
+                // the dual residual carries O(eps/mu) multiplier noise, required to 1e4*tol
+                st_here = rdmax <= 1e4 * Pr.tol * (1.0 + sd) ? MPC_OK : MPC_NUMERICAL;
+                it = iter;
+                done = true;
                 break;
             }
-            // acceptable iterate, returned if the iteration later breaks down
-            if (rdmax <= 1e4 * P.tol * (1.0 + sd) && rpmax <= 10.0 * P.tol * (1.0 + bscale) && mu <= 1e2 * P.tol_mu) {
-                double inf = 0.0;
-                if (live) {
-#pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
-                        if ((j == 6 || j == 7) && !has_obs) continue;
-                        if (S.rxi[j * NP + k] > 1e-6 * (1.0 + fabs(S.bs[NROW * k + j]))) inf = 1.0;
-                    }
-                    acc0 = S.du[2 * lane];
-                    acc1 = S.du[2 * lane + 1];
-                }
-                inf_acc = wave_max(inf) > 0.0;
-                have_acc = true;
-            }
-            if (mu < 1e-3 * P.tol_mu) { st_here = MPC_NUMERICAL; ++it; break; }
             // -- barrier weights, augmented stage Hessians ---------------------------------------
-            if (live) {
-                double Qp[10];
+            double il[R], inu[R], wv[R], ilb[RB], wb[RB];
+            {
+                double Qp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                for (int a = 0; a < 10; ++a) Qp[a] = S.Qs[10 * k + a];
-#pragma unroll
-                for (int j = 0; j < NROW; ++j) {
-                    if ((j == 6 || j == 7) && !has_obs) continue;
-                    double c[4];
-                    row_coef(j, hL, P.L, P.tgap, c);
-                    double d = S.rs[j * NP + k] / S.rl[j * NP + k] + S.rxi[j * NP + k] / S.rnu[j * NP + k];
-                    double w = 1.0 / d;
+                for (int s = 0; s < R; ++s) {
+                    il[s] = frcp(rl[s]);
+                    inu[s] = frcp(rnu[s]);
+                    wv[s] = ron[s] ? frcp(fma(rs[s], il[s], rxi[s] * inu[s])) : 0.0;   // 1/d
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
-                        for (int cc = a; cc < 4; ++cc)
-                            if (c[a] != 0.0 && c[cc] != 0.0) Qp[p4(a, cc)] = fma(w * c[a], c[cc], Qp[p4(a, cc)]);
+                        for (int c = a; c < 4; ++c) Qp[p4(a, c)] = fma(wv[s] * cf[s][a], cf[s][c], Qp[p4(a, c)]);
+                }
+                double r0 = 0.0, r1 = 0.0;
+#pragma unroll
+                for (int s = 0; s < RB; ++s) {
+                    ilb[s] = frcp(lb[s]);
+                    wb[s] = bon[s] ? lb[s] * frcp(sb[s]) : 0.0;
+                    if (bj[s] < 2) r0 += wb[s]; else r1 += wb[s];
                 }
 #pragma unroll
-                for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a];
-                double r0 = R0, r1 = R1;
+                for (int a = 0; a < 10; ++a) Qp[a] = stage_sum(Qp[a]);
+                r0 = stage_sum(r0);
+                r1 = stage_sum(r1);
+                if (lead) {
+                    double Qs[10], qs[4];
+                    stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
-                for (int j = 0; j < NBOX; ++j) {
-                    double w = S.blv[j * N + lane] / S.bsv[j * N + lane];
-                    if (j < 2) r0 += w; else r1 += w;
+                    for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a] + Qs[a];
+                    S.Rt[2 * (k - 1)] = R0 + r0;
+                    S.Rt[2 * (k - 1) + 1] = R1 + r1;
                 }
-                S.Rt[2 * lane] = r0;
-                S.Rt[2 * lane + 1] = r1;
             }
             wave_sync();
-            riccati_factor(S, N, dt, lane);
-            // -- predictor and corrector solves ----------------------------------------------------
-            double sig = 0.0, alpha = 0.0;
-            for (int pass = 0; pass < 2; ++pass) {
-                const double smu = (pass == 1) ? sig * mu : 0.0;
-                if (live) {
-                    double x4[4];
+            riccati_factor(S, G, N, dt, ln);
+            // -- predictor, corrector (and, if needed, centred) solves ---------------------------------
+            double p4v[R], p5v[R], pbv[RB];
+            double sig = 0.0;
+            bool applied = false;
+#pragma unroll 1
+            for (int pass = 0; pass < 3; ++pass) {
+                // pass 0: affine predictor; 1: Mehrotra corrector; 2: plain centred direction, taken when
+                // the corrector would not reduce complementarity (oracle: comp_after > comp)
+                const double smu = (pass >= 1) ? sig * mu : 0.0;
+                double r4[R], r5[R], r4b[RB], rh[R], rhb[RB];
+                {
+                    double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) x4[a] = S.Xr[5 * k + st4(a)];
-                    double q4[4];
+                    for (int s = 0; s < R; ++s) {
+                        r4[s] = rs[s] * rl[s] - smu;
+                        r5[s] = rxi[s] * rnu[s] - smu;
+                        if (pass == 1) { r4[s] += p4v[s]; r5[s] += p5v[s]; }
+                        const double rp = dot4(cf[s], x4) + rxi[s] - rs[s] - bk[s];
+                        const double rx = rho - rl[s] - rnu[s];
+                        rh[s] = -rp - r4[s] * il[s] + fma(rxi[s], rx, r5[s]) * inu[s];
+                        const double w = ron[s] ? rh[s] * wv[s] : 0.0;
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) q4[a] = -(S.ys[4 * k + a] + S.ya[4 * k + a]);
-#pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
-                        if ((j == 6 || j == 7) && !has_obs) continue;
-                        double c[4];
-                        row_coef(j, hL, P.L, P.tgap, c);
-                        const double sv = S.rs[j * NP + k], lv = S.rl[j * NP + k];
-                        const double xv = S.rxi[j * NP + k], nv = S.rnu[j * NP + k];
-                        double r4 = sv * lv, r5 = xv * nv;
-                        if (pass == 1) { r4 += S.pa4[j * NP + k] - smu; r5 += S.pa5[j * NP + k] - smu; }
-                        double rp = c[0] * x4[0] + c[1] * x4[1] + c[2] * x4[2] + c[3] * x4[3] + xv - sv -
-                                    S.bs[NROW * k + j];
-                        double rx = rho - lv - nv;
-                        double d = sv / lv + xv / nv;
-                        double rh = -rp - r4 / lv + (r5 + xv * rx) / nv;
-                        double w = rh / d;
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) q4[a] = fma(c[a], w, q4[a]);
+                        for (int a = 0; a < 4; ++a) q4[a] = fma(cf[s][a], w, q4[a]);
                     }
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) S.qh[4 * k + a] = q4[a];
-                    const double du0 = S.du[2 * lane], du1 = S.du[2 * lane + 1];
-                    double g0 = -(S.zs[2 * lane] + S.za[2 * lane]);
-                    double g1 = -(S.zs[2 * lane + 1] + S.za[2 * lane + 1]);
-#pragma unroll
-                    for (int j = 0; j < NBOX; ++j) {
-                        const double sb = S.bsv[j * N + lane], lb = S.blv[j * N + lane];
-                        double r4 = sb * lb;
-                        if (pass == 1) r4 += S.pab[j * N + lane] - smu;
-                        double uu = (j < 2) ? du0 : du1;
-                        double rp = bsign(j) * uu - sb - S.bb[4 * lane + j];
-                        double rh = -rp - r4 / lb;
-                        double v = bsign(j) * rh * lb / sb;
-                        if (j < 2) g0 += v; else g1 += v;
+                    for (int s = 0; s < RB; ++s) {
+                        r4b[s] = sb[s] * lb[s] - smu;
+                        if (pass == 1) r4b[s] += pbv[s];
+                        const double rp = bsign(bj[s]) * ((bj[s] < 2) ? du0 : du1) - sb[s] - bb[s];
+                        rhb[s] = -rp - r4b[s] * ilb[s];
+                        const double v = bsign(bj[s]) * rhb[s] * wb[s];
+                        if (bj[s] < 2) g0 += v; else g1 += v;
                     }
-                    S.gh[2 * lane] = g0;
-                    S.gh[2 * lane + 1] = g1;
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) q4[a] = stage_sum(q4[a]);
+                    g0 = stage_sum(g0);
+                    g1 = stage_sum(g1);
+                    if (lead) {
+#pragma unroll
+                        for (int a = 0; a < 4; ++a) S.qh[4 * k + a] = q4[a] - (S.yc[4 * k + a] + S.ya[4 * k + a]);
+                        S.gh[2 * (k - 1)] = g0 - (S.zc[2 * (k - 1)] + S.za[2 * (k - 1)]);
+                        S.gh[2 * (k - 1) + 1] = g1 - (S.zc[2 * (k - 1) + 1] + S.za[2 * (k - 1) + 1]);
+                    }
                 }
                 wave_sync();
-                riccati_solve(S, N, dt, lane);
-                // row directions and step length
+                riccati_solve(S, N, dt, ln);
+                // row directions and the step length
+                double dsv[R], dlv[R], dxv[R], dnv[R], dsb[RB], dlb[RB];
                 double amax = 1.0;
-                if (live) {
-                    double x4[4], dx4[4];
+                {
+                    double dx4[4];
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) { x4[a] = S.Xr[5 * k + st4(a)]; dx4[a] = S.dX[5 * k + st4(a)]; }
+                    for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
 #pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
-                        if ((j == 6 || j == 7) && !has_obs) continue;
-                        double c[4];
-                        row_coef(j, hL, P.L, P.tgap, c);
-                        const double sv = S.rs[j * NP + k], lv = S.rl[j * NP + k];
-                        const double xv = S.rxi[j * NP + k], nv = S.rnu[j * NP + k];
-                        double r4 = sv * lv, r5 = xv * nv;
-                        if (pass == 1) { r4 += S.pa4[j * NP + k] - smu; r5 += S.pa5[j * NP + k] - smu; }
-                        double rp = c[0] * x4[0] + c[1] * x4[1] + c[2] * x4[2] + c[3] * x4[3] + xv - sv -
-                                    S.bs[NROW * k + j];
-                        double rx = rho - lv - nv;
-                        double d = sv / lv + xv / nv;
-                        double rh = -rp - r4 / lv + (r5 + xv * rx) / nv;
-                        double cdx = c[0] * dx4[0] + c[1] * dx4[1] + c[2] * dx4[2] + c[3] * dx4[3];
-                        double dl = (rh - cdx) / d;
-                        double ds = -(r4 + sv * dl) / lv;
-                        double dn = rx - dl;
-                        double dxi = -(r5 + xv * dn) / nv;
-                        if (pass == 0) {
-                            // affine step: remember the second-order products for the corrector
-                            S.pa4[j * NP + k] = ds * dl;
-                            S.pa5[j * NP + k] = dxi * dn;
-                            S.tl[j * NP + k] = ds;     // scratch: affine directions for mu_aff
-                            S.cls[j * NP + k] = dl;
-                        } else {
-                            // stash the corrector direction in pa4/pa5/tl/cls until alpha is known
-                            S.pa4[j * NP + k] = ds;
-                            S.pa5[j * NP + k] = dl;
-                            S.tl[j * NP + k] = dxi;
-                            S.cls[j * NP + k] = dn;
-                        }
-                        if (ds < 0.0) amax = fmin(amax, -sv / ds);
-                        if (dl < 0.0) amax = fmin(amax, -lv / dl);
-                        if (dxi < 0.0) amax = fmin(amax, -xv / dxi);
-                        if (dn < 0.0) amax = fmin(amax, -nv / dn);
-                        if (pass == 0) {
-                            // keep dxi, dn for mu_aff in registers-free form: recomputed below
-                        }
+                    for (int s = 0; s < R; ++s) {
+                        const double rx = rho - rl[s] - rnu[s];
+                        const double dl = (rh[s] - dot4(cf[s], dx4)) * wv[s];
+                        const double ds = -fma(rs[s], dl, r4[s]) * il[s];
+                        const double dn = rx - dl;
+                        const double dxi = -fma(rxi[s], dn, r5[s]) * inu[s];
+                        dsv[s] = ds; dlv[s] = dl; dxv[s] = dxi; dnv[s] = dn;
+                        if (!ron[s]) continue;
+                        if (ds < 0.0) amax = fmin(amax, -rs[s] / ds);
+                        if (dl < 0.0) amax = fmin(amax, -rl[s] / dl);
+                        if (dxi < 0.0) amax = fmin(amax, -rxi[s] / dxi);
+                        if (dn < 0.0) amax = fmin(amax, -rnu[s] / dn);
                     }
-                    const double du0 = S.du[2 * lane], du1 = S.du[2 * lane + 1];
-                    const double dd0 = S.dud[2 * lane], dd1 = S.dud[2 * lane + 1];
+                    const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
 #pragma unroll
-                    for (int j = 0; j < NBOX; ++j) {
-                        const double sb = S.bsv[j * N + lane], lb = S.blv[j * N + lane];
-                        double r4 = sb * lb;
-                        if (pass == 1) r4 += S.pab[j * N + lane] - smu;
-                        double uu = (j < 2) ? du0 : du1;
-                        double duu = (j < 2) ? dd0 : dd1;
-                        double rp = bsign(j) * uu - sb - S.bb[4 * lane + j];
-                        double rh = -rp - r4 / lb;
-                        double dl = (rh - bsign(j) * duu) * lb / sb;
-                        double ds = -(r4 + sb * dl) / lb;
-                        if (pass == 0) S.pab[j * N + lane] = ds * dl;
-                        else { S.tlb[j * N + lane] = ds; S.cls[9 * NP + j * N + lane] = dl; }
-                        if (pass == 0) { S.tlb[j * N + lane] = ds; S.cls[9 * NP + j * N + lane] = dl; }
-                        if (ds < 0.0) amax = fmin(amax, -sb / ds);
-                        if (dl < 0.0) amax = fmin(amax, -lb / dl);
+                    for (int s = 0; s < RB; ++s) {
+                        const double duu = (bj[s] < 2) ? dd0 : dd1;
+                        const double dl = (rhb[s] - bsign(bj[s]) * duu) * wb[s];
+                        const double ds = -fma(sb[s], dl, r4b[s]) * ilb[s];
+                        dsb[s] = ds; dlb[s] = dl;
+                        if (!bon[s]) continue;
+                        if (ds < 0.0) amax = fmin(amax, -sb[s] / ds);
+                        if (dl < 0.0) amax = fmin(amax, -lb[s] / dl);
                     }
                 }
-                amax = wave_min(amax);
+                amax = G.min(amax);
+                // complementarity after the step (pass 0: at the full affine step length)
+                const double a_try = (pass == 0) ? amax : fmin(1.0, TAU * amax);
+                double ca = 0.0;
+#pragma unroll
+                for (int s = 0; s < R; ++s)
+                    if (ron[s])
+                        ca += fma(a_try, dsv[s], rs[s]) * fma(a_try, dlv[s], rl[s]) +
+                              fma(a_try, dxv[s], rxi[s]) * fma(a_try, dnv[s], rnu[s]);
+#pragma unroll
+                for (int s = 0; s < RB; ++s)
+                    if (bon[s]) ca += fma(a_try, dsb[s], sb[s]) * fma(a_try, dlb[s], lb[s]);
+                ca = G.sum(ca);
                 if (pass == 0) {
-                    // mu after the affine step (needs dxi, dn: recomputed from the stored products)
-                    double ca = 0.0;
-                    if (live) {
-                        double x4[4], dx4[4];
+                    const double r = ca / comp;
+                    sig = r * r * r;
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) { x4[a] = S.Xr[5 * k + st4(a)]; dx4[a] = S.dX[5 * k + st4(a)]; }
+                    for (int s = 0; s < R; ++s) { p4v[s] = dsv[s] * dlv[s]; p5v[s] = dxv[s] * dnv[s]; }
 #pragma unroll
-                        for (int j = 0; j < NROW; ++j) {
-                            if ((j == 6 || j == 7) && !has_obs) continue;
-                            const double sv = S.rs[j * NP + k], lv = S.rl[j * NP + k];
-                            const double xv = S.rxi[j * NP + k], nv = S.rnu[j * NP + k];
-                            const double ds = S.tl[j * NP + k], dl = S.cls[j * NP + k];
-                            double dn = (rho - lv - nv) - dl;
-                            double dxi = -(xv * nv + xv * dn) / nv;
-                            ca += fma(amax, ds, sv) * fma(amax, dl, lv) + fma(amax, dxi, xv) * fma(amax, dn, nv);
-                        }
-#pragma unroll
-                        for (int j = 0; j < NBOX; ++j)
-                            ca += fma(amax, S.tlb[j * N + lane], S.bsv[j * N + lane]) *
-                                  fma(amax, S.cls[9 * NP + j * N + lane], S.blv[j * N + lane]);
-                    }
-                    ca = wave_sum(ca);
-                    double mua = ca / Mtot;
-                    sig = mua / mu;
-                    sig = sig * sig * sig;
-                } else {
-                    alpha = fmin(1.0, TAU * amax);
-                    if (live) {
-#pragma unroll
-                        for (int j = 0; j < NROW; ++j) {
-                            if ((j == 6 || j == 7) && !has_obs) continue;
-                            const int o = j * NP + k;
-                            S.rs[o] = fma(alpha, S.pa4[o], S.rs[o]);
-                            S.rl[o] = fma(alpha, S.pa5[o], S.rl[o]);
-                            S.rxi[o] = fma(alpha, S.tl[o], S.rxi[o]);
-                            S.rnu[o] = fma(alpha, S.cls[o], S.rnu[o]);
-                        }
-#pragma unroll
-                        for (int j = 0; j < NBOX; ++j) {
-                            const int o = j * N + lane;
-                            S.bsv[o] = fma(alpha, S.tlb[o], S.bsv[o]);
-                            S.blv[o] = fma(alpha, S.cls[9 * NP + o], S.blv[o]);
-                        }
-                        S.du[2 * lane] = fma(alpha, S.dud[2 * lane], S.du[2 * lane]);
-                        S.du[2 * lane + 1] = fma(alpha, S.dud[2 * lane + 1], S.du[2 * lane + 1]);
-                    }
+                    for (int s = 0; s < RB; ++s) pbv[s] = dsb[s] * dlb[s];
+                    continue;
                 }
-                wave_sync();
+                if (pass == 1 && ca > comp) continue;     // safeguard: take the centred direction
+                const double alpha = a_try;
+                applied = true;
+                stall = (mu < 1e-6 && ca > 0.9 * comp) ? stall + 1 : 0;
+#pragma unroll
+                for (int s = 0; s < R; ++s) {
+                    if (!ron[s]) continue;
+                    rs[s] = fma(alpha, dsv[s], rs[s]);
+                    rl[s] = fma(alpha, dlv[s], rl[s]);
+                    rxi[s] = fma(alpha, dxv[s], rxi[s]);
+                    rnu[s] = fma(alpha, dnv[s], rnu[s]);
+                }
+#pragma unroll
+                for (int s = 0; s < RB; ++s) {
+                    if (!bon[s]) continue;
+                    sb[s] = fma(alpha, dsb[s], sb[s]);
+                    lb[s] = fma(alpha, dlb[s], lb[s]);
+                }
+                if (ln < N) {
+                    S.du[2 * ln] = fma(alpha, S.dud[2 * ln], S.du[2 * ln]);
+                    S.du[2 * ln + 1] = fma(alpha, S.dud[2 * ln + 1], S.du[2 * ln + 1]);
+                }
+                break;
             }
-            stall = (alpha < 1e-10) ? stall + 1 : 0;
-            if (stall >= 3) { st_here = MPC_NUMERICAL; ++it; break; }
+            (void)applied;
+            wave_sync();
+            it = iter + 1;
+            if (stall >= 5) { st_here = MPC_NUMERICAL; done = true; break; }
         }
+        (void)done;
         total_it += it;
-        const bool use_acc = (st_here != MPC_OK) && have_acc;
-        if (use_acc && live) { S.du[2 * lane] = acc0; S.du[2 * lane + 1] = acc1; }
-        wave_sync();
+        // NaN guard and the infeasibility flag
         double bad = 0.0;
-        if (live) bad = (S.du[2 * lane] == S.du[2 * lane] && S.du[2 * lane + 1] == S.du[2 * lane + 1]) ? 0.0 : 1.0;
-        bad = wave_max(bad);
+        if (ln < N) bad = (S.du[2 * ln] == S.du[2 * ln] && S.du[2 * ln + 1] == S.du[2 * ln + 1]) ? 0.0 : 1.0;
+        bad = G.max(bad);
         if (bad > 0.0) {
             st_here = MPC_NUMERICAL;
-            if (live) { S.du[2 * lane] = 0.0; S.du[2 * lane + 1] = 0.0; }
-        } else if (use_acc) {
-            st_here = inf_acc ? MPC_INFEASIBLE : MPC_OK;
+            if (ln < N) { S.du[2 * ln] = 0.0; S.du[2 * ln + 1] = 0.0; }
         } else if (st_here == MPC_OK) {
             double inf = 0.0;
-            if (live) {
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) {
-                    if ((j == 6 || j == 7) && !has_obs) continue;
-                    if (S.rxi[j * NP + k] > 1e-6 * (1.0 + fabs(S.bs[NROW * k + j]))) inf = 1.0;
-                }
-            }
-            if (wave_max(inf) > 0.0) st_here = MPC_INFEASIBLE;
+            for (int s = 0; s < R; ++s)
+                if (ron[s] && rxi[s] > 1e-6 * (1.0 + fabs(bk[s]))) inf = 1.0;
+            if (G.max(inf) > 0.0) st_here = MPC_INFEASIBLE;
         }
         wave_sync();
 
         // ---- active-set polish (oracle polish()) --------------------------
-        if (P.polish && bad == 0.0) {
-            // classification from the interior-point iterate: 0 inactive, 1 active, 2 violated
-            if (live) {
+        if (Pr.polish && bad == 0.0) {
+            // class per row: 0 inactive, 1 active (equality), 2 violated (multiplier fixed at rho)
+            int cls[R], clb[RB];
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) {
-                    const int o = j * NP + k;
-                    double c = 0.0;
-                    if ((j != 6 && j != 7) || has_obs) {
-                        if (S.rxi[o] > S.rnu[o]) c = 2.0;
-                        else if (S.rl[o] > S.rs[o]) c = 1.0;
-                    }
-                    S.cls[o] = c;
-                }
+            for (int s = 0; s < R; ++s) cls[s] = !ron[s] ? 0 : (rxi[s] > rnu[s] ? 2 : (rl[s] > rs[s] ? 1 : 0));
 #pragma unroll
-                for (int j = 0; j < NBOX; ++j) {
-                    const int o = j * N + lane;
-                    S.cls[9 * NP + o] = S.blv[o] > S.bsv[o] ? 1.0 : 0.0;
-                }
-                S.dub[2 * lane] = S.du[2 * lane];
-                S.dub[2 * lane + 1] = S.du[2 * lane + 1];
-            }
+            for (int s = 0; s < RB; ++s) clb[s] = (bon[s] && lb[s] > sb[s]) ? 1 : 0;
+            if (ln < N) { S.dub[2 * ln] = S.du[2 * ln]; S.dub[2 * ln + 1] = S.du[2 * ln + 1]; }
             wave_sync();
             bool accepted = false;
             double nviol_acc = 0.0;
-            for (int round = 0; round < POLISH_ROUNDS && !accepted; ++round) {
-                if (live) {
-                    S.du[2 * lane] = S.dub[2 * lane];
-                    S.du[2 * lane + 1] = S.dub[2 * lane + 1];
-                    double Qp[10];
+            for (int round = 0; round < POLISH_ROUNDS; ++round) {
+                double tl[R], tlb[RB];
+                {
+                    if (ln < N) { S.du[2 * ln] = S.dub[2 * ln]; S.du[2 * ln + 1] = S.dub[2 * ln + 1]; }
+                    double Qp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                    for (int a = 0; a < 10; ++a) Qp[a] = S.Qs[10 * k + a];
+                    for (int s = 0; s < R; ++s) {
+                        tl[s] = rl[s];
+                        const double w = cls[s] == 1 ? 1.0 / POLISH_DELTA : 0.0;
 #pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
-                        const int o = j * NP + k;
-                        S.tl[o] = S.rl[o];
-                        if (S.cls[o] == 1.0) {
-                            double c[4];
-                            row_coef(j, hL, P.L, P.tgap, c);
+                        for (int a = 0; a < 4; ++a)
 #pragma unroll
-                            for (int a = 0; a < 4; ++a)
+                            for (int c = a; c < 4; ++c) Qp[p4(a, c)] = fma(w * cf[s][a], cf[s][c], Qp[p4(a, c)]);
+                    }
+                    double r0 = 0.0, r1 = 0.0;
 #pragma unroll
-                                for (int cc = a; cc < 4; ++cc)
-                                    if (c[a] != 0.0 && c[cc] != 0.0)
-                                        Qp[p4(a, cc)] = fma(c[a] / POLISH_DELTA, c[cc], Qp[p4(a, cc)]);
-                        }
+                    for (int s = 0; s < RB; ++s) {
+                        tlb[s] = lb[s];
+                        if (clb[s] == 1) { if (bj[s] < 2) r0 += 1.0 / POLISH_DELTA; else r1 += 1.0 / POLISH_DELTA; }
                     }
 #pragma unroll
-                    for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a];
-                    double r0 = R0, r1 = R1;
+                    for (int a = 0; a < 10; ++a) Qp[a] = stage_sum(Qp[a]);
+                    r0 = stage_sum(r0);
+                    r1 = stage_sum(r1);
+                    if (lead) {
+                        double Qs[10], qs[4];
+                        stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
-                    for (int j = 0; j < NBOX; ++j) {
-                        const int o = j * N + lane;
-                        S.tlb[o] = S.blv[o];
-                        if (S.cls[9 * NP + o] == 1.0) { if (j < 2) r0 += 1.0 / POLISH_DELTA; else r1 += 1.0 / POLISH_DELTA; }
+                        for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a] + Qs[a];
+                        S.Rt[2 * (k - 1)] = R0 + r0;
+                        S.Rt[2 * (k - 1) + 1] = R1 + r1;
                     }
-                    S.Rt[2 * lane] = r0;
-                    S.Rt[2 * lane + 1] = r1;
                 }
                 wave_sync();
-                riccati_factor(S, N, dt, lane);
+                riccati_factor(S, G, N, dt, ln);
+                double x4[4];
+#pragma unroll 1
                 for (int r = 0; r <= POLISH_REFINE; ++r) {
-                    rollout_lin(S, N, dt, S.du, S.Xr, lane);
+                    rollout_lin(S, N, dt, S.du, S.dX, ln);
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) x4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
                     if (r == POLISH_REFINE) break;
                     // exact KKT residual of the equality QP -> LQR right-hand side
-                    if (live) {
-                        double x4[4];
+                    double r2[R], r2b[RB];
+                    const double du0 = live ? S.du[2 * (k - 1)] : 0.0, du1 = live ? S.du[2 * (k - 1) + 1] : 0.0;
+                    {
+                        double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) x4[a] = S.Xr[5 * k + st4(a)];
-                        double q4[4];
+                        for (int s = 0; s < R; ++s) {
+                            r2[s] = (cls[s] == 1) ? bk[s] - dot4(cf[s], x4) : 0.0;
+                            const double wgt = (cls[s] == 2) ? rho : (cls[s] == 1 ? tl[s] + r2[s] * (1.0 / POLISH_DELTA) : 0.0);
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) {
-                            double acc = S.qs[4 * k + a];
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) acc = fma(S.Qs[10 * k + p4(a, c)], x4[c], acc);
-                            q4[a] = -acc;
+                            for (int a = 0; a < 4; ++a) q4[a] = fma(cf[s][a], wgt, q4[a]);
                         }
 #pragma unroll
-                        for (int j = 0; j < NROW; ++j) {
-                            const int o = j * NP + k;
-                            const double cl = S.cls[o];
-                            if (cl == 0.0) continue;
-                            double c[4];
-                            row_coef(j, hL, P.L, P.tgap, c);
-                            double lam = (cl == 2.0) ? rho : S.tl[o];
-                            double r2 = 0.0;
-                            if (cl == 1.0) r2 = S.bs[NROW * k + j] - (c[0] * x4[0] + c[1] * x4[1] + c[2] * x4[2] + c[3] * x4[3]);
-#pragma unroll
-                            for (int a = 0; a < 4; ++a) q4[a] = fma(c[a], lam + r2 / POLISH_DELTA, q4[a]);
-                            S.pa4[o] = r2;
+                        for (int s = 0; s < RB; ++s) {
+                            const double uu = (bj[s] < 2) ? du0 : du1;
+                            r2b[s] = (clb[s] == 1) ? bb[s] - bsign(bj[s]) * uu : 0.0;
+                            const double v = (clb[s] == 1) ? bsign(bj[s]) * (tlb[s] + r2b[s] * (1.0 / POLISH_DELTA)) : 0.0;
+                            if (bj[s] < 2) g0 += v; else g1 += v;
                         }
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) S.qh[4 * k + a] = q4[a];
-                        const double du0 = S.du[2 * lane], du1 = S.du[2 * lane + 1];
-                        double g0 = -fma(R0, du0, S.rr[2 * lane]);
-                        double g1 = -fma(R1, du1, S.rr[2 * lane + 1]);
+                        for (int a = 0; a < 4; ++a) q4[a] = stage_sum(q4[a]);
+                        g0 = stage_sum(g0);
+                        g1 = stage_sum(g1);
+                        if (lead) {
+                            double Qs[10], qs[4];
+                            stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
-                        for (int j = 0; j < NBOX; ++j) {
-                            const int o = j * N + lane;
-                            if (S.cls[9 * NP + o] != 1.0) continue;
-                            double uu = (j < 2) ? du0 : du1;
-                            double r2 = S.bb[4 * lane + j] - bsign(j) * uu;
-                            double v = bsign(j) * (S.tlb[o] + r2 / POLISH_DELTA);
-                            if (j < 2) g0 += v; else g1 += v;
-                            S.pab[o] = r2;
+                            for (int a = 0; a < 4; ++a) {
+                                double acc = qs[a];
+#pragma unroll
+                                for (int c = 0; c < 4; ++c) acc = fma(Qs[p4(a, c)], x4[c], acc);
+                                S.qh[4 * k + a] = q4[a] - acc;
+                            }
+                            S.gh[2 * (k - 1)] = g0 - fma(R0, du0, R0 * S.ub[2 * (k - 1)]);
+                            S.gh[2 * (k - 1) + 1] = g1 - fma(R1, du1, R1 * S.ub[2 * (k - 1) + 1]);
                         }
-                        S.gh[2 * lane] = g0;
-                        S.gh[2 * lane + 1] = g1;
                     }
                     wave_sync();
-                    riccati_solve(S, N, dt, lane);
-                    if (live) {
+                    riccati_solve(S, N, dt, ln);
+                    {
                         double dx4[4];
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) dx4[a] = S.dX[5 * k + st4(a)];
+                        for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
 #pragma unroll
-                        for (int j = 0; j < NROW; ++j) {
-                            const int o = j * NP + k;
-                            if (S.cls[o] != 1.0) continue;
-                            double c[4];
-                            row_coef(j, hL, P.L, P.tgap, c);
-                            double cdx = c[0] * dx4[0] + c[1] * dx4[1] + c[2] * dx4[2] + c[3] * dx4[3];
-                            S.tl[o] += (S.pa4[o] - cdx) / POLISH_DELTA;
-                        }
-                        const double dd0 = S.dud[2 * lane], dd1 = S.dud[2 * lane + 1];
+                        for (int s = 0; s < R; ++s)
+                            if (cls[s] == 1) tl[s] += (r2[s] - dot4(cf[s], dx4)) * (1.0 / POLISH_DELTA);
+                        const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
 #pragma unroll
-                        for (int j = 0; j < NBOX; ++j) {
-                            const int o = j * N + lane;
-                            if (S.cls[9 * NP + o] != 1.0) continue;
-                            double duu = (j < 2) ? dd0 : dd1;
-                            S.tlb[o] += (S.pab[o] - bsign(j) * duu) / POLISH_DELTA;
-                        }
-                        S.du[2 * lane] += dd0;
-                        S.du[2 * lane + 1] += dd1;
+                        for (int s = 0; s < RB; ++s)
+                            if (clb[s] == 1)
+                                tlb[s] += (r2b[s] - bsign(bj[s]) * ((bj[s] < 2) ? dd0 : dd1)) * (1.0 / POLISH_DELTA);
                     }
+                    wave_sync();
+                    if (ln < N) { S.du[2 * ln] += S.dud[2 * ln]; S.du[2 * ln + 1] += S.dud[2 * ln + 1]; }
                     wave_sync();
                 }
                 // acceptance: KKT consistency; otherwise flip every offending row and retry
                 double lmax = 1.0;
-                if (live) {
 #pragma unroll
-                    for (int j = 0; j < NROW; ++j)
-                        if (S.cls[j * NP + k] == 1.0) lmax = fmax(lmax, fabs(S.tl[j * NP + k]));
+                for (int s = 0; s < R; ++s)
+                    if (cls[s] == 1) lmax = fmax(lmax, fabs(tl[s]));
 #pragma unroll
-                    for (int j = 0; j < NBOX; ++j)
-                        if (S.cls[9 * NP + j * N + lane] == 1.0) lmax = fmax(lmax, fabs(S.tlb[j * N + lane]));
-                }
-                lmax = wave_max(lmax);
+                for (int s = 0; s < RB; ++s)
+                    if (clb[s] == 1) lmax = fmax(lmax, fabs(tlb[s]));
+                lmax = G.max(lmax);
                 double worst = 0.0, nviol = 0.0, finite = 1.0;
-                if (live) {
-                    double x4[4];
+                bool flip[R], flipb[RB];
+                {
+                    const double du0 = live ? S.du[2 * (k - 1)] : 0.0, du1 = live ? S.du[2 * (k - 1) + 1] : 0.0;
+                    if (!(du0 == du0) || !(du1 == du1)) finite = 0.0;
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) x4[a] = S.Xr[5 * k + st4(a)];
-#pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
-                        if ((j == 6 || j == 7) && !has_obs) continue;
-                        const int o = j * NP + k;
-                        double c[4];
-                        row_coef(j, hL, P.L, P.tgap, c);
-                        const double bj = S.bs[NROW * k + j];
-                        const double bsc = 1.0 + fabs(bj);
-                        const double r = (c[0] * x4[0] + c[1] * x4[1] + c[2] * x4[2] + c[3] * x4[3]) - bj;
-                        const double cl = S.cls[o];
+                    for (int s = 0; s < R; ++s) {
+                        flip[s] = false;
+                        if (!ron[s]) continue;
+                        const double bsc = 1.0 + fabs(bk[s]);
+                        const double r = dot4(cf[s], x4) - bk[s];
                         double badv = 0.0;
-                        if (cl == 1.0) {
-                            const double l = S.tl[o];
-                            if (l < -1e-9 * lmax) badv = -l / lmax;
-                            else if (l > rho * (1.0 + 1e-9)) badv = (l - rho) / lmax;
+                        if (cls[s] == 1) {
+                            if (tl[s] < -1e-9 * lmax) badv = -tl[s] / lmax;
+                            else if (tl[s] > rho * (1.0 + 1e-9)) badv = (tl[s] - rho) / lmax;
                             else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
-                        } else if (cl == 2.0) {
+                        } else if (cls[s] == 2) {
                             if (r > 1e-9 * bsc) badv = r / bsc;
                             if (r < -1e-6 * bsc) nviol += 1.0;
                         } else if (r < -1e-9 * bsc) badv = -r / bsc;
                         worst = fmax(worst, badv);
-                        S.pa5[o] = badv;        // offending-row flag for the flip below
+                        flip[s] = badv > 0.0;
                     }
-                    const double du0 = S.du[2 * lane], du1 = S.du[2 * lane + 1];
-                    if (!(du0 == du0) || !(du1 == du1)) finite = 0.0;
 #pragma unroll
-                    for (int j = 0; j < NBOX; ++j) {
-                        const int o = j * N + lane;
-                        const double bj = S.bb[4 * lane + j];
-                        const double bsc = 1.0 + fabs(bj);
-                        const double r = bsign(j) * ((j < 2) ? du0 : du1) - bj;
+                    for (int s = 0; s < RB; ++s) {
+                        flipb[s] = false;
+                        if (!bon[s]) continue;
+                        const double bsc = 1.0 + fabs(bb[s]);
+                        const double r = bsign(bj[s]) * ((bj[s] < 2) ? du0 : du1) - bb[s];
                         double badv = 0.0;
-                        if (S.cls[9 * NP + o] == 1.0) {
-                            if (S.tlb[o] < -1e-9 * lmax) badv = -S.tlb[o] / lmax;
+                        if (clb[s] == 1) {
+                            if (tlb[s] < -1e-9 * lmax) badv = -tlb[s] / lmax;
                             else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
                         } else if (r < -1e-9 * bsc) badv = -r / bsc;
                         worst = fmax(worst, badv);
-                        S.pab[o] = badv;
+                        flipb[s] = badv > 0.0;
                     }
                 }
-                worst = wave_max(worst);
-                nviol = wave_sum(nviol);
-                finite = wave_min(finite);
+                worst = G.max(worst);
+                nviol = G.sum(nviol);
+                finite = G.min(finite);
                 if (finite == 0.0) break;
                 if (worst == 0.0) {
                     accepted = true;
                     nviol_acc = nviol;
-                } else if (live) {
-#pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
-                        if ((j == 6 || j == 7) && !has_obs) continue;
-                        const int o = j * NP + k;
-                        if (S.pa5[o] > 0.0) {
-                            const double cl = S.cls[o];
-                            S.cls[o] = (cl == 1.0) ? (S.tl[o] > rho ? 2.0 : 0.0) : 1.0;
-                        }
-                    }
-#pragma unroll
-                    for (int j = 0; j < NBOX; ++j) {
-                        const int o = j * N + lane;
-                        if (S.pab[o] > 0.0) S.cls[9 * NP + o] = (S.cls[9 * NP + o] == 1.0) ? 0.0 : 1.0;
-                    }
+                    if (ln < N) { S.dub[2 * ln] = S.du[2 * ln]; S.dub[2 * ln + 1] = S.du[2 * ln + 1]; }
+                    wave_sync();
+                    break;
                 }
+#pragma unroll
+                for (int s = 0; s < R; ++s)
+                    if (flip[s]) cls[s] = (cls[s] == 1) ? (tl[s] > rho ? 2 : 0) : 1;
+#pragma unroll
+                for (int s = 0; s < RB; ++s)
+                    if (flipb[s]) clb[s] = 1 - clb[s];
                 wave_sync();
             }
-            if (accepted) {
-                st_here = nviol_acc > 0.0 ? MPC_INFEASIBLE : MPC_OK;
-            } else if (live) {
-                S.du[2 * lane] = S.dub[2 * lane];
-                S.du[2 * lane + 1] = S.dub[2 * lane + 1];
-            }
+            // the accepted polish (or, if none, the interior-point iterate) is in dub
+            if (ln < N) { S.du[2 * ln] = S.dub[2 * ln]; S.du[2 * ln + 1] = S.dub[2 * ln + 1]; }
+            if (accepted) st_here = nviol_acc > 0.0 ? MPC_INFEASIBLE : MPC_OK;
             wave_sync();
         }
         status = st_here;
-        if (live) {
-            S.ub[2 * lane] += S.du[2 * lane];
-            S.ub[2 * lane + 1] += S.du[2 * lane + 1];
+        if (ln < N) {
+            S.ub[2 * ln] += S.du[2 * ln];
+            S.ub[2 * ln + 1] += S.du[2 * ln + 1];
         }
         wave_sync();
     }
 
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------
-    predict_wave(tab, P, x0, S.ub, S.xb, S.kap, lane);
-    if (live && Ug) {
-        Ug[(size_t)b * 2 * N + 2 * lane] = S.ub[2 * lane];
-        Ug[(size_t)b * 2 * N + 2 * lane + 1] = S.ub[2 * lane + 1];
+    predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, ln);
+    if (ln < N && Ug) {
+        Ug[(size_t)b * 2 * N + 2 * ln] = S.ub[2 * ln];
+        Ug[(size_t)b * 2 * N + 2 * ln + 1] = S.ub[2 * ln + 1];
     }
     if (Xg)
-        for (int i = lane; i < 5 * NP; i += WAVE) Xg[(size_t)b * 5 * NP + i] = S.xb[i];
-    if (lane == 0) {
+        for (int i = ln; i < 5 * NP; i += WAVE) Xg[(size_t)b * 5 * NP + i] = S.Xr[i];
+    if (ln == 0) {
         if (u0g) { u0g[2 * (size_t)b] = S.ub[0]; u0g[2 * (size_t)b + 1] = S.ub[1]; }
         if (statusg) statusg[b] = status;
         if (itersg) itersg[b] = total_it;
@@ -1237,7 +1195,7 @@ extern "C" void mpc_default_params(mpc_params* p) {
     p->sqp_iters = 1;
     p->max_iter = 80;
     p->tol = 1e-9;
-    p->tol_mu = 1e-12;
+    p->tol_mu = 1e-10;
     p->elastic_rho = 1e5;
     p->polish = 1;
 }
@@ -1263,7 +1221,6 @@ static KParams kparams(const mpc_params* p) {
     k.linearization = p->linearization;
     k.sqp_iters = p->sqp_iters;
     k.max_iter = p->max_iter;
-    k.polish = p->polish;
     k.dt = p->dt;
     k.u_min0 = p->u_min[0]; k.u_min1 = p->u_min[1];
     k.u_max0 = p->u_max[0]; k.u_max1 = p->u_max[1];
@@ -1277,6 +1234,7 @@ static KParams kparams(const mpc_params* p) {
     k.tol = p->tol;
     k.tol_mu = p->tol_mu;
     k.rho = p->elastic_rho;
+    k.polish = p->polish;
     return k;
 }
 
@@ -1386,8 +1344,18 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
     size_t lds = sizeof(double) * (size_t)lds_doubles(kp.N);
     if (lds > 160 * 1024) return fail(MPC_E_ARG, "horizon too long for LDS");
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
-    hipLaunchKernelGGL(mpc_solve_kernel, dim3(B), dim3(WAVE), lds, (hipStream_t)stream, c->tab, kp, B, x0,
-                       obs, obs ? n_obs : nullptr, ubar, u0, U, Xpred, status, iters);
+    // rows of a stage spread over P lanes: all 64 lanes carry row state when N is short
+    const int* nob = obs ? n_obs : nullptr;
+    hipStream_t st = (hipStream_t)stream;
+    if (3 * kp.N <= WAVE)
+        hipLaunchKernelGGL(mpc_solve_kernel<3>, dim3(B), dim3(WAVE), lds, st, c->tab, kp, B, x0, obs, nob, ubar, u0,
+                           U, Xpred, status, iters);
+    else if (2 * kp.N <= WAVE)
+        hipLaunchKernelGGL(mpc_solve_kernel<2>, dim3(B), dim3(WAVE), lds, st, c->tab, kp, B, x0, obs, nob, ubar, u0,
+                           U, Xpred, status, iters);
+    else
+        hipLaunchKernelGGL(mpc_solve_kernel<1>, dim3(B), dim3(WAVE), lds, st, c->tab, kp, B, x0, obs, nob, ubar, u0,
+                           U, Xpred, status, iters);
     HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
     return MPC_SUCCESS;
 }
