@@ -139,22 +139,19 @@ struct Lds {
     double* kk;    // [N][2]
     double* Xr;    // [N+1][5]  rollout of the current iterate
     double* dX;    // [N+1][5]  rollout of the direction
-    double* du;    // [N][2]    current iterate dU
     double* dud;   // [N][2]    direction dU
-    double* dub;   // [N][2]    interior-point iterate kept during the polish
     double* yc;    // [N+1][4]  dual-residual stage terms: cost part
     double* ya;    // [N+1][4]  dual-residual stage terms: multiplier part
     double* zc;    // [N][2]
     double* za;    // [N][2]
     double* ub;    // [N][2]    linearisation point
-    double* xb;    // [N+1][5]  nominal rollout / predict output
     double* kap;   // [N+1]     k_ref(xbar_k); then shat_k (min obstacle prediction)
 };
 
 __host__ __device__ inline int lds_doubles(int N) {
     int NP = N + 1;
     return N * 5 + NP * 6 + NP * 10 + N * 2 + N * 10 + N * 3 + NP * 4 + N * 2 + N * 2 + NP * 5 + NP * 5 + N * 2 +
-           N * 2 + N * 2 + NP * 4 + NP * 4 + N * 2 + N * 2 + N * 2 + NP * 5 + NP;
+           NP * 4 + NP * 4 + N * 2 + N * 2 + N * 2 + NP;
 }
 
 __device__ inline Lds carve(double* p, int N) {
@@ -171,15 +168,12 @@ __device__ inline Lds carve(double* p, int N) {
     L.kk = p; p += N * 2;
     L.Xr = p; p += NP * 5;
     L.dX = p; p += NP * 5;
-    L.du = p; p += N * 2;
     L.dud = p; p += N * 2;
-    L.dub = p; p += N * 2;
     L.yc = p; p += NP * 4;
     L.ya = p; p += NP * 4;
     L.zc = p; p += N * 2;
     L.za = p; p += N * 2;
     L.ub = p; p += N * 2;
-    L.xb = p; p += NP * 5;
     L.kap = p; p += NP;
     return L;
 }
@@ -299,124 +293,197 @@ __device__ __forceinline__ void applyAT(const double* a, double dt, const double
     y[4] = fma(dt, m[0], fma(a[1], m[1], fma(a[4], m[2], m[4])));
 }
 
-// X = G u : rollout of the linear model from x_0 = 0 (group-uniform; lane 0 of the group writes)
-__device__ void rollout_lin(const Lds& S, int N, double dt, const double* u, double* X, int ln) {
-    if (ln == 0) {
-        double x[5] = {0, 0, 0, 0, 0};
-        for (int a = 0; a < 5; ++a) X[a] = 0.0;
-        for (int j = 0; j < N; ++j) {
-            double y[5];
-            applyA(S.A5 + 5 * j, dt, x, y);
-            y[3] = fma(dt, u[2 * j], y[3]);
-            y[4] = fma(dt, u[2 * j + 1], y[4]);
-            for (int a = 0; a < 5; ++a) { x[a] = y[a]; X[5 * (j + 1) + a] = y[a]; }
-        }
-    }
-    wave_sync();
+// packed symmetric 5x5 on (s,d,o,k,v): index of (i,j)
+__host__ __device__ constexpr int s5(int i, int j) {
+    return i <= j ? i * 5 - i * (i - 1) / 2 + (j - i) : j * 5 - j * (j - 1) / 2 + (i - j);
 }
 
-// Riccati factorisation of  min sum 0.5 x'Qt x + 0.5 u'Rt u,  x_{t+1} = A_t x_t + B u_t,  x_0 = 0,
-// spread over 25 lanes of the group: lane (i, j) = ln / 5, ln % 5 holds P[i][j].  Per stage:
-// M = P A (gather row i of P), S = Rt + B'P B = Ls Ls' (uniform), W = Ls^-1 B'M, K = -Ls^-T W,
-// P <- Qt + A'M - W'W (gather column j of M), symmetrised.  The Cholesky form keeps ~2 more digits
-// than an explicit S^-1 once barrier weights reach 1e12.
-template <int GL>
-__device__ void riccati_factor(const Lds& S, const Grp<GL>& G, int N, double dt, int ln) {
-    const int i = ln / 5, j = ln - 5 * (ln / 5);
-    const bool act = ln < 25;
-    const int ri = i == 4 ? 3 : i, rj = j == 4 ? 3 : j;
-    const bool qv = act && i != 3 && j != 3;
-    const int qo = qv ? p4(ri, rj) : 0;
-    double P = qv ? S.Qt[10 * N + qo] : 0.0;
+// Riccati factorisation of  min sum 0.5 x'Qt x + 0.5 u'Rt u,  x_{t+1} = A_t x_t + B u_t,  x_0 = 0.
+// The recursion is inherently sequential over stages; it is run wave-uniformly (every lane holds the
+// same P in registers, so no cross-lane traffic sits on the critical path), with the next stage's A_t
+// and Rt prefetched from LDS one step ahead.  Per stage: M = P A, S = Rt + B'P B = Ls Ls',
+// W = Ls^-1 B'M, K = -Ls^-T W, P <- Qt + A'M - W'W (upper triangle).  The Cholesky form keeps ~2 more
+// digits than an explicit S^-1 once barrier weights reach 1e12.
+// Restates riccati_factor() of oracle/mpc_oracle.c.
+__device__ void riccati_factor(const Lds& S, int N, double dt, int ln) {
+    double P[15];
+#pragma unroll
+    for (int i = 0; i < 15; ++i) P[i] = 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = a; c < 4; ++c) P[s5(st4(a), st4(c))] = S.Qt[10 * N + p4(a, c)];
     const double dt2 = dt * dt;
+    double na[5], nr0, nr1;
+#pragma unroll
+    for (int a = 0; a < 5; ++a) na[a] = S.A5[5 * (N - 1) + a];
+    nr0 = S.Rt[2 * (N - 1)];
+    nr1 = S.Rt[2 * (N - 1) + 1];
     for (int t = N - 1; t >= 0; --t) {
-        const double* a = S.A5 + 5 * t;
-        const double a12 = a[0], a14 = a[1], a20 = a[2], a23 = a[3], a24 = a[4];
-        const double r0 = S.Rt[2 * t], r1 = S.Rt[2 * t + 1];
-        const double qt = (qv && t >= 1) ? S.Qt[10 * t + qo] : 0.0;
-        // M[i][j] = P[i][j] + sum_l P[i][l] J'[l][j]
-        const double p0 = G.get(P, 5 * i + 0), p1 = G.get(P, 5 * i + 1), p2 = G.get(P, 5 * i + 2);
-        double M = P;
-        if (j == 0) M = fma(p2, a20, M);
-        else if (j == 2) M = fma(p1, a12, M);
-        else if (j == 3) M = fma(p2, a23, M);
-        else if (j == 4) M = fma(p0, dt, fma(p1, a14, fma(p2, a24, M)));
-        // S = Rt + dt^2 P[{3,4},{3,4}]  (uniform)
-        const double P33 = G.get(P, 18), P34 = G.get(P, 19), P44 = G.get(P, 24);
-        double s00 = fma(dt2, P33, r0), s01 = dt2 * P34, s11 = fma(dt2, P44, r1);
+        const double a12 = na[0], a14 = na[1], a20 = na[2], a23 = na[3], a24 = na[4];
+        const double r0 = nr0, r1 = nr1;
+        const int tn = t >= 1 ? t - 1 : 0;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) na[a] = S.A5[5 * tn + a];
+        nr0 = S.Rt[2 * tn];
+        nr1 = S.Rt[2 * tn + 1];
+        double q[10];
+#pragma unroll
+        for (int a = 0; a < 10; ++a) q[a] = S.Qt[10 * t + a];   // used at the end of the step
+        // S = Rt + dt^2 P[{3,4},{3,4}] and its Cholesky factor
+        double s00 = fma(dt2, P[s5(3, 3)], r0), s01 = dt2 * P[s5(3, 4)], s11 = fma(dt2, P[s5(4, 4)], r1);
         if (!(s00 > 0.0)) s00 = 1e-300 + fabs(s00);
         const double l00 = sqrt(s00), il00 = frcp(l00), l10 = s01 * il00;
         double r11 = s11 - l10 * l10;
         if (!(r11 > 1e-14 * s11)) r11 = 1e-14 * fabs(s11) + 1e-300;
         const double l11 = sqrt(r11), il11 = frcp(l11);
-        // column j of M, and M[3][i], M[4][i]
-        const double m0 = G.get(M, j), m1 = G.get(M, 5 + j), m2 = G.get(M, 10 + j);
-        const double m3 = G.get(M, 15 + j), m4 = G.get(M, 20 + j);
-        const double mi3 = G.get(M, 15 + i), mi4 = G.get(M, 20 + i);
-        const double W0j = dt * m3 * il00, W1j = (dt * m4 - l10 * W0j) * il11;
-        const double W0i = dt * mi3 * il00, W1i = (dt * mi4 - l10 * W0i) * il11;
-        if (act && i == 0) {
-            const double K1 = -W1j * il11;
-            const double K0 = -(W0j + l10 * K1) * il00;
-            S.Kf[10 * t + j] = K0;
-            S.Kf[10 * t + 5 + j] = K1;
+        // M = P A  (A = I + J', J' sparse: a12, a14, a20, a23, a24, dt)
+        double M[5][5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const double pi0 = P[s5(i, 0)], pi1 = P[s5(i, 1)], pi2 = P[s5(i, 2)], pi3 = P[s5(i, 3)],
+                         pi4 = P[s5(i, 4)];
+            M[i][0] = fma(pi2, a20, pi0);
+            M[i][1] = pi1;
+            M[i][2] = fma(pi1, a12, pi2);
+            M[i][3] = fma(pi2, a23, pi3);
+            M[i][4] = fma(pi0, dt, fma(pi1, a14, fma(pi2, a24, pi4)));
         }
-        if (ln == 0) { S.Si[3 * t] = il00; S.Si[3 * t + 1] = l10; S.Si[3 * t + 2] = il11; }
-        // (A'M)[i][j] = M[i][j] + sum_l J'[l][i] M[l][j]
-        double Nij = M;
-        if (i == 0) Nij = fma(a20, m2, Nij);
-        else if (i == 2) Nij = fma(a12, m1, Nij);
-        else if (i == 3) Nij = fma(a23, m2, Nij);
-        else if (i == 4) Nij = fma(dt, m0, fma(a14, m1, fma(a24, m2, Nij)));
-        const double Pn = Nij - fma(W0i, W0j, W1i * W1j);
-        const double Pt = G.get(Pn, 5 * j + i);
-        P = act ? 0.5 * (Pn + Pt) + qt : 0.0;
+        double W0[5], W1[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            W0[j] = dt * M[3][j] * il00;
+            W1[j] = (dt * M[4][j] - l10 * W0[j]) * il11;
+        }
+        if (ln == 0) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const double K1 = -W1[j] * il11;
+                S.Kf[10 * t + 5 + j] = K1;
+                S.Kf[10 * t + j] = -(W0[j] + l10 * K1) * il00;
+            }
+            S.Si[3 * t] = il00;
+            S.Si[3 * t + 1] = l10;
+            S.Si[3 * t + 2] = il11;
+        }
+        if (t >= 1) {
+            // P <- (A'M)  + Qt - W'W, (A'M)[i][j] = M[i][j] + sum_l J'[l][i] M[l][j]
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+#pragma unroll
+                for (int j = i; j < 5; ++j) {
+                    double v = M[i][j];
+                    if (i == 0) v = fma(a20, M[2][j], v);
+                    else if (i == 2) v = fma(a12, M[1][j], v);
+                    else if (i == 3) v = fma(a23, M[2][j], v);
+                    else if (i == 4) v = fma(dt, M[0][j], fma(a14, M[1][j], fma(a24, M[2][j], v)));
+                    v -= fma(W0[i], W0[j], W1[i] * W1[j]);
+                    if (i != 3 && j != 3) v += q[p4(i == 4 ? 3 : i, j == 4 ? 3 : j)];
+                    P[s5(i, j)] = v;
+                }
+        }
     }
     wave_sync();
 }
 
 // LQR solve with the factorisation: linear terms -qh (stages 1..N), -gh (controls).
-// Writes dud (controls) and dX (states, x_0 = 0).  Group-uniform; lane 0 of the group writes.
+// Writes dud (controls) and dX (states, x_0 = 0).  Group-uniform; the stage data of the next step is
+// loaded into the other of two register buffers while the current step computes (ping-pong, so the
+// LDS latency hides behind the dependent FP64 chain); lane 0 of the group writes.
+// Restates riccati_solve() of oracle/mpc_oracle.c.
+struct BwdBuf { double g[2], si[3], a[5], K[10], q[4]; };
+struct FwdBuf { double kk[2], K[10], a[5]; };
+
+__device__ __forceinline__ void load_bwd(const Lds& S, int t, BwdBuf& B) {
+    B.g[0] = S.gh[2 * t];
+    B.g[1] = S.gh[2 * t + 1];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) B.si[a] = S.Si[3 * t + a];
+#pragma unroll
+    for (int a = 0; a < 5; ++a) B.a[a] = S.A5[5 * t + a];
+#pragma unroll
+    for (int a = 0; a < 10; ++a) B.K[a] = S.Kf[10 * t + a];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) B.q[a] = S.qh[4 * t + a];
+}
+__device__ __forceinline__ void load_fwd(const Lds& S, int t, FwdBuf& F) {
+    F.kk[0] = S.kk[2 * t];
+    F.kk[1] = S.kk[2 * t + 1];
+#pragma unroll
+    for (int a = 0; a < 10; ++a) F.K[a] = S.Kf[10 * t + a];
+#pragma unroll
+    for (int a = 0; a < 5; ++a) F.a[a] = S.A5[5 * t + a];
+}
+// one backward step: p <- A_t'p + K_t'h + qh_t  (t >= 1), kk_t = S_t^-1 h,  h = gh_t + B'p
+__device__ __forceinline__ void bwd_step(const Lds& S, int t, double dt, const BwdBuf& B, double p5[5], int ln) {
+    const double h0 = fma(dt, p5[3], B.g[0]);
+    const double h1 = fma(dt, p5[4], B.g[1]);
+    const double w0 = h0 * B.si[0];
+    const double w1 = (h1 - B.si[1] * w0) * B.si[2];
+    const double k1 = w1 * B.si[2];
+    const double k0 = (w0 - B.si[1] * k1) * B.si[0];
+    if (ln == 0) { S.kk[2 * t] = k0; S.kk[2 * t + 1] = k1; }
+    if (t >= 1) {
+        double pa[5];
+        applyAT(B.a, dt, p5, pa);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) pa[st4(a)] += B.q[a];
+#pragma unroll
+        for (int a = 0; a < 5; ++a) p5[a] = fma(B.K[a], h0, fma(B.K[5 + a], h1, pa[a]));
+    }
+}
+// one forward step: u_t = kk_t + K_t x_t,  x_{t+1} = A_t x_t + B u_t
+__device__ __forceinline__ void fwd_step(const Lds& S, int t, double dt, const FwdBuf& F, double x[5], int ln) {
+    double v0 = fma(F.K[0], x[0], fma(F.K[1], x[1], F.kk[0]));
+    double v1 = fma(F.K[5], x[0], fma(F.K[6], x[1], F.kk[1]));
+    v0 = fma(F.K[2], x[2], v0) + fma(F.K[3], x[3], F.K[4] * x[4]);
+    v1 = fma(F.K[7], x[2], v1) + fma(F.K[8], x[3], F.K[9] * x[4]);
+    double y[5];
+    applyA(F.a, dt, x, y);
+    y[3] = fma(dt, v0, y[3]);
+    y[4] = fma(dt, v1, y[4]);
+#pragma unroll
+    for (int a = 0; a < 5; ++a) x[a] = y[a];
+    if (ln == 0) {
+        S.dud[2 * t] = v0;
+        S.dud[2 * t + 1] = v1;
+#pragma unroll
+        for (int a = 0; a < 5; ++a) S.dX[5 * (t + 1) + a] = y[a];
+    }
+}
+
 __device__ void riccati_solve(const Lds& S, int N, double dt, int ln) {
     double p5[5] = {0, 0, 0, 0, 0};
 #pragma unroll
     for (int a = 0; a < 4; ++a) p5[st4(a)] = S.qh[4 * N + a];
-    for (int t = N - 1; t >= 0; --t) {
-        double h0 = fma(dt, p5[3], S.gh[2 * t]);
-        double h1 = fma(dt, p5[4], S.gh[2 * t + 1]);
-        const double* si = S.Si + 3 * t;
-        double w0 = h0 * si[0];
-        double w1 = (h1 - si[1] * w0) * si[2];
-        double k1 = w1 * si[2];
-        double k0 = (w0 - si[1] * k1) * si[0];
-        if (ln == 0) { S.kk[2 * t] = k0; S.kk[2 * t + 1] = k1; }
-        if (t >= 1) {
-            double pa[5];
-            applyAT(S.A5 + 5 * t, dt, p5, pa);
-            const double* K = S.Kf + 10 * t;
-#pragma unroll
-            for (int a = 0; a < 5; ++a) p5[a] = fma(K[a], h0, fma(K[5 + a], h1, pa[a]));
-#pragma unroll
-            for (int a = 0; a < 4; ++a) p5[st4(a)] += S.qh[4 * t + a];
+    {
+        BwdBuf A, B;
+        load_bwd(S, N - 1, A);
+        int t = N - 1;
+        while (true) {
+            load_bwd(S, t >= 1 ? t - 1 : 0, B);      // unconditional: keeps the LDS wait counts exact
+            bwd_step(S, t, dt, A, p5, ln);
+            if (--t < 0) break;
+            load_bwd(S, t >= 1 ? t - 1 : 0, A);
+            bwd_step(S, t, dt, B, p5, ln);
+            if (--t < 0) break;
         }
     }
     wave_sync();
-    if (ln == 0) {
-        double x[5] = {0, 0, 0, 0, 0};
+    if (ln == 0)
         for (int a = 0; a < 5; ++a) S.dX[a] = 0.0;
-        for (int t = 0; t < N; ++t) {
-            const double* K = S.Kf + 10 * t;
-            double v0 = S.kk[2 * t], v1 = S.kk[2 * t + 1];
-#pragma unroll
-            for (int a = 0; a < 5; ++a) { v0 = fma(K[a], x[a], v0); v1 = fma(K[5 + a], x[a], v1); }
-            S.dud[2 * t] = v0;
-            S.dud[2 * t + 1] = v1;
-            double y[5];
-            applyA(S.A5 + 5 * t, dt, x, y);
-            y[3] = fma(dt, v0, y[3]);
-            y[4] = fma(dt, v1, y[4]);
-#pragma unroll
-            for (int a = 0; a < 5; ++a) { x[a] = y[a]; S.dX[5 * (t + 1) + a] = y[a]; }
+    {
+        double x[5] = {0, 0, 0, 0, 0};
+        FwdBuf A, B;
+        load_fwd(S, 0, A);
+        int t = 0;
+        while (true) {
+            load_fwd(S, t + 1 < N ? t + 1 : t, B);
+            fwd_step(S, t, dt, A, x, ln);
+            if (++t >= N) break;
+            load_fwd(S, t + 1 < N ? t + 1 : t, A);
+            fwd_step(S, t, dt, B, x, ln);
+            if (++t >= N) break;
         }
     }
     wave_sync();
@@ -469,42 +536,64 @@ __device__ __forceinline__ void stage_cost(const double* cst, double wd, double 
     }
 }
 
+// phase-cycle instrumentation of a diagnostic build (-DMPC_PROF, tools/phase_probe.py); compiled
+// out of the product library
+#ifdef MPC_PROF
+__device__ unsigned long long g_prof[16];
+#define PROF_DECL                                \
+    unsigned long long prof_acc[12];             \
+    for (int i_ = 0; i_ < 12; ++i_) prof_acc[i_] = 0; \
+    unsigned long long prof_t = __builtin_amdgcn_s_memtime();
+#define PROF(i)                                                  \
+    {                                                            \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+        prof_acc[i] += t_ - prof_t;                              \
+        prof_t = t_;                                             \
+    }
+#define PROF_END \
+    if (gl == 0 && bvalid) for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_prof[i_], prof_acc[i_]);
+#else
+#define PROF_DECL
+#define PROF(i)
+#define PROF_END
+#endif
+
 #define POLISH_DELTA 1e-11
 #define POLISH_REFINE 4
 #define POLISH_ROUNDS 6
 #define MU0 1.0
 
-// Row slots: the 9 soft rows and 4 box rows of a stage are spread over P lanes (part = lane % P):
-// lane slot s holds soft row j = part * R + s (if < 9) and box row part * RB + s (if < 4).
-template <int P>
-struct Parts {
-    static constexpr int R = (NROW + P - 1) / P;
-    static constexpr int RB = (NBOX + P - 1) / P;
-};
-
 // ------------------------------------------------------------------------------------------
-// the solver kernel: one wavefront per MPC instance; stage k = 1..N is owned by the P lanes
-// (k-1)*P .. (k-1)*P+P-1 (control t = k-1 with it); 25 lanes run the Riccati factorisation;
-// the vector recursions run wave-uniformly from LDS.
+// the solver kernel.  A 64-lane wavefront carries G = 64 / GL MPC instances, one per aligned group
+// of GL lanes (GL = 16, 32 or 64, the smallest with N + 1 <= GL).  Within a group, lane k-1 owns
+// stage k = 1..N: its 9 soft rows and the 4 box rows of control k-1, whose interior-point state
+// lives in that lane's registers (row ids are compile-time, so the row coefficients fold away).
+// The stage-wise recursions (Riccati factorisation and solves, rollouts) run group-uniformly
+// from the group's LDS region: one instruction stream serves G instances, which is what pays for
+// the inherently sequential part of the algorithm on a 64-wide SIMD.
+// All branching is group-uniform, so a group that has converged simply drops out of the exec mask.
 // ------------------------------------------------------------------------------------------
-template <int P>
+template <int GL>
 __global__ void __launch_bounds__(WAVE)
 mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g, const double* __restrict__ obsg,
                  const int* __restrict__ nobsg, const double* __restrict__ ubarg, double* __restrict__ u0g,
                  double* __restrict__ Ug, double* __restrict__ Xg, int* __restrict__ statusg,
                  int* __restrict__ itersg) {
-    constexpr int R = Parts<P>::R, RB = Parts<P>::RB;
+    constexpr int G = WAVE / GL;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int b = blockIdx.x;
-    if (b >= B) return;
     const int ln = threadIdx.x;
-    const Grp<WAVE> G{0};
+    const int grp = ln / GL, gl = ln % GL;
+    int b = blockIdx.x * G + grp;
+    const bool bvalid = b < B;
+    if (!bvalid) b = B - 1;          // a spare group repeats the last instance; its outputs are dropped
+    PROF_DECL
+    const Grp<GL> Q{grp * GL};
     const int N = Pr.N;
     const int NP = N + 1;
     const double dt = Pr.dt;
     const double rho = Pr.rho;
     const double hL = Pr.L / 2.0;
-    Lds S = carve(smem, N);
+    Lds S = carve(smem + (size_t)grp * lds_doubles(N), N);
 
     double x0[5];
 #pragma unroll
@@ -514,57 +603,35 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     const double* obs = obsg ? obsg + (size_t)b * Pr.max_obs * 2 : nullptr;
     const bool has_obs = nobs > 0;
 
-    // stage ownership
-    const int part = ln % P;
-    const int k = ln / P + 1;                 // stage of this lane
-    const bool live = k <= N;                 // lane owns rows of stage k (and boxes of control k-1)
-    const int sbase = ln - part;              // first lane of this stage
-    const bool lead = live && part == 0;      // writes the stage sums
-
-    // row slots of this lane
-    int rj[R];
-    bool ron[R];
-    double cf[R][4];
+    const int k = gl + 1;            // stage of this lane
+    const bool live = k <= N;        // lane owns the rows of stage k and the boxes of control k-1
+    bool ron[NROW];
+    double cf[NROW][4];
 #pragma unroll
-    for (int s = 0; s < R; ++s) {
-        rj[s] = part * R + s;
-        ron[s] = live && rj[s] < NROW && ((rj[s] != 6 && rj[s] != 7) || has_obs);
-        row_coef(rj[s] < NROW ? rj[s] : 0, hL, Pr.L, Pr.tgap, cf[s]);
+    for (int j = 0; j < NROW; ++j) {
+        ron[j] = live && ((j != 6 && j != 7) || has_obs);
+        row_coef(j, hL, Pr.L, Pr.tgap, cf[j]);
     }
-    int bj[RB];
-    bool bon[RB];
-#pragma unroll
-    for (int s = 0; s < RB; ++s) {
-        bj[s] = part * RB + s;
-        bon[s] = live && bj[s] < NBOX;
-    }
-    // sum of a per-lane partial over the P lanes of the stage (valid on the stage's part-0 lane)
-    auto stage_sum = [&](double v) {
-        double r = v;
-#pragma unroll
-        for (int q = 1; q < P; ++q) r += G.get(v, sbase + q);
-        return r;
-    };
 
     // ---- K1: linearisation point ---------------------------------------------------------
-    if (ln < N) {
+    if (gl < N) {
         if (ubarg) {
-            S.ub[2 * ln] = ubarg[(size_t)b * 2 * N + 2 * ln];
-            S.ub[2 * ln + 1] = ubarg[(size_t)b * 2 * N + 2 * ln + 1];
+            S.ub[2 * gl] = ubarg[(size_t)b * 2 * N + 2 * gl];
+            S.ub[2 * gl + 1] = ubarg[(size_t)b * 2 * N + 2 * gl + 1];
         } else {
             // warm start, trajectory_tracking.py:224-246: s_curr advanced by repeated addition,
-            // sticky brake flag over steps 0..ln
+            // sticky brake flag over steps 0..gl
             double s_curr = x0[0], v_curr = x0[4];
             bool brake = false;
-            for (int j = 0; j <= ln; ++j) {
+            for (int j = 0; j <= gl; ++j) {
                 if (j > 0) s_curr += v_curr * dt;
                 for (int i = 0; i < nobs; ++i)
                     if ((obs[2 * i] - s_curr) < Pr.brake_distance) brake = true;
             }
             double ur[2];
             get_control(tab, s_curr, ur);
-            S.ub[2 * ln] = ur[0];
-            S.ub[2 * ln + 1] = brake ? Pr.brake_accel : ur[1];
+            S.ub[2 * gl] = ur[0];
+            S.ub[2 * gl + 1] = brake ? Pr.brake_accel : ur[1];
         }
     }
     wave_sync();
@@ -578,25 +645,26 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     int status = MPC_OK, total_it = 0;
     for (int sqp = 0; sqp < nsqp; ++sqp) {
         // ---- K1: nominal rollout == predict(x0, ubar), into Xr ------------------------------
-        predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, ln);
+        predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
         // ---- K2: stage data of QP(ubar) ----------------------------------------------------
         const bool gn = Pr.linearization != 0;
         double refk[5], slk[4];
-        if (ln <= N) get_state(tab, S.Xr[5 * ln], refk, slk);
-        if (ln < N) {
-            const double* x = S.Xr + 5 * ln;
+        if (gl <= N) get_state(tab, S.Xr[5 * gl], refk, slk);
+        if (gl < N) {
+            const double* x = S.Xr + 5 * gl;
             double dk = gn ? slk[2] : 0.0;
-            S.A5[5 * ln + 0] = dt * x[4];
-            S.A5[5 * ln + 1] = dt * x[2];
-            S.A5[5 * ln + 2] = dt * (-x[4] * dk);
-            S.A5[5 * ln + 3] = dt * x[4];
-            S.A5[5 * ln + 4] = dt * (x[3] - refk[3]);
+            S.A5[5 * gl + 0] = dt * x[4];
+            S.A5[5 * gl + 1] = dt * x[2];
+            S.A5[5 * gl + 2] = dt * (-x[4] * dk);
+            S.A5[5 * gl + 3] = dt * x[4];
+            S.A5[5 * gl + 4] = dt * (x[3] - refk[3]);
         }
-        // cost data of stage k (lookups done by lane k)
+        // cost data of stage k (lookups done by lane k of the group)
         {
-            const double rk1 = G.get(refk[1], k), rk2 = G.get(refk[2], k), rk4 = G.get(refk[4], k);
-            const double sk0 = G.get(slk[0], k), sk1 = G.get(slk[1], k), sk3 = G.get(slk[3], k);
-            if (lead) {
+            const int src = k < GL ? k : GL - 1;
+            const double rk1 = Q.get(refk[1], src), rk2 = Q.get(refk[2], src), rk4 = Q.get(refk[4], src);
+            const double sk0 = Q.get(slk[0], src), sk1 = Q.get(slk[1], src), sk3 = Q.get(slk[3], src);
+            if (live) {
                 const double* x = S.Xr + 5 * k;
                 S.cst[6 * k + 0] = gn ? -sk0 : 0.0;
                 S.cst[6 * k + 1] = gn ? -sk1 : 0.0;
@@ -606,8 +674,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 S.cst[6 * k + 5] = x[4] - rk4;
             }
         }
-        // row bounds of this lane's rows, box bounds of its boxes
-        double bk[R], bb[RB];
+        // row bounds of stage k, box bounds of control k-1
+        double bk[NROW], bb[NBOX];
         double bscale_l = 0.0;
         {
             double shat = INFINITY;
@@ -619,99 +687,82 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             const double* x = S.Xr + 5 * (live ? k : 0);
             const double sl = Pr.sl;
             const double pv0 = x[1], pv1 = x[1] + hL * x[2], pv2 = x[1] + Pr.L * x[2];
+            double v[NROW];
+            v[0] = -sl - pv0;
+            v[1] = -(sl - pv0);
+            v[2] = -sl - pv1;
+            v[3] = -(sl - pv1);
+            v[4] = -sl - pv2;
+            v[5] = -(sl - pv2);
+            v[6] = has_obs ? -(shat - Pr.osd - x[0]) : 0.0;
+            v[7] = has_obs ? -(shat - x[0] - Pr.tgap * x[4]) : 0.0;
+            v[8] = -x[4];
 #pragma unroll
-            for (int s = 0; s < R; ++s) {
-                const int j = rj[s];
-                double v = 0.0;
-                switch (j) {
-                    case 0: v = -sl - pv0; break;
-                    case 1: v = -(sl - pv0); break;
-                    case 2: v = -sl - pv1; break;
-                    case 3: v = -(sl - pv1); break;
-                    case 4: v = -sl - pv2; break;
-                    case 5: v = -(sl - pv2); break;
-                    case 6: v = has_obs ? -(shat - Pr.osd - x[0]) : 0.0; break;
-                    case 7: v = has_obs ? -(shat - x[0] - Pr.tgap * x[4]) : 0.0; break;
-                    case 8: v = -x[4]; break;
-                    default: v = 0.0; break;
-                }
-                bk[s] = ron[s] ? v : 0.0;
-                bscale_l = fmax(bscale_l, fabs(bk[s]));
+            for (int j = 0; j < NROW; ++j) {
+                bk[j] = ron[j] ? v[j] : 0.0;
+                bscale_l = fmax(bscale_l, fabs(bk[j]));
             }
             const double ub0 = live ? S.ub[2 * (k - 1)] : 0.0, ub1 = live ? S.ub[2 * (k - 1) + 1] : 0.0;
+            bb[0] = live ? Pr.u_min0 - ub0 : 0.0;
+            bb[1] = live ? -(Pr.u_max0 - ub0) : 0.0;
+            bb[2] = live ? Pr.u_min1 - ub1 : 0.0;
+            bb[3] = live ? -(Pr.u_max1 - ub1) : 0.0;
 #pragma unroll
-            for (int s = 0; s < RB; ++s) {
-                double v = 0.0;
-                switch (bj[s]) {
-                    case 0: v = Pr.u_min0 - ub0; break;
-                    case 1: v = -(Pr.u_max0 - ub0); break;
-                    case 2: v = Pr.u_min1 - ub1; break;
-                    case 3: v = -(Pr.u_max1 - ub1); break;
-                    default: v = 0.0; break;
-                }
-                bb[s] = bon[s] ? v : 0.0;
-                bscale_l = fmax(bscale_l, fabs(bb[s]));
-            }
+            for (int j = 0; j < NBOX; ++j) bscale_l = fmax(bscale_l, fabs(bb[j]));
         }
-        const double bscale = G.max(bscale_l);
+        const double bscale = Q.max(bscale_l);
         wave_sync();
 
         // ---- K4: PDIP; interior-point state of this lane's rows in registers ---------------------
-        double rs[R], rl[R], rxi[R], rnu[R], sb[RB], lb[RB];
+        double rs[NROW], rl[NROW], rxi[NROW], rnu[NROW], sb[NBOX], lb[NBOX];
 #pragma unroll
-        for (int s = 0; s < R; ++s) {
+        for (int j = 0; j < NROW; ++j) {
             // centred start: xi covers the violation, s*lam = MU0 with lam <= rho/2, nu = rho - lam
-            const double r0 = -bk[s];
+            const double r0 = -bk[j];
             const double xi = (r0 < 0 ? -r0 : 0.0) + XI0;
             const double sv = r0 + xi;
             const double lam = fmin(MU0 * frcp(sv), 0.5 * rho);
-            rxi[s] = xi; rs[s] = sv; rl[s] = lam; rnu[s] = rho - lam;
+            rxi[j] = xi; rs[j] = sv; rl[j] = lam; rnu[j] = rho - lam;
         }
 #pragma unroll
-        for (int s = 0; s < RB; ++s) {
-            const double r0 = -bb[s];
-            sb[s] = r0 > 1.0 ? r0 : 1.0;
-            lb[s] = 1.0;
+        for (int j = 0; j < NBOX; ++j) {
+            const double r0 = -bb[j];
+            sb[j] = r0 > 1.0 ? r0 : 1.0;
+            lb[j] = 1.0;
         }
-        if (ln < N) { S.du[2 * ln] = 0.0; S.du[2 * ln + 1] = 0.0; }
-        wave_sync();
-
         int it = 0, st_here = MPC_MAX_ITER, stall = 0;
-        bool done = false;
         double mu = 0.0;
+        // x4: state of stage k along the current iterate, G du (du = 0 at the start); updated with the
+        // state direction of every step, so the linear rollout never re-runs (it is linear in du)
+        double x4[4] = {0.0, 0.0, 0.0, 0.0};
+        double du0 = 0.0, du1 = 0.0;        // control k-1 of the current iterate
+        PROF(0)
         for (int iter = 0; iter < Pr.max_iter; ++iter) {
-            rollout_lin(S, N, dt, S.du, S.dX, ln);
+            PROF(1)
             // -- stage-parallel residuals ------------------------------------------------------
-            double x4[4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a) x4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
-            const double du0 = live ? S.du[2 * (k - 1)] : 0.0, du1 = live ? S.du[2 * (k - 1) + 1] : 0.0;
             double rpmax = 0.0, rxmax = 0.0, comp = 0.0;
-            double ya[4] = {0, 0, 0, 0}, za0 = 0.0, za1 = 0.0;
+            double ya[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int s = 0; s < R; ++s) {
-                if (!ron[s]) continue;
-                const double rp = dot4(cf[s], x4) + rxi[s] - rs[s] - bk[s];
-                const double rx = rho - rl[s] - rnu[s];
+            for (int j = 0; j < NROW; ++j) {
+                if (!ron[j]) continue;
+                const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
+                const double rx = rho - rl[j] - rnu[j];
 #pragma unroll
-                for (int a = 0; a < 4; ++a) ya[a] = fma(-rl[s], cf[s][a], ya[a]);
+                for (int a = 0; a < 4; ++a) ya[a] = fma(-rl[j], cf[j][a], ya[a]);
                 rpmax = fmax(rpmax, fabs(rp));
                 rxmax = fmax(rxmax, fabs(rx));
-                comp = fma(rs[s], rl[s], fma(rxi[s], rnu[s], comp));
+                comp = fma(rs[j], rl[j], fma(rxi[j], rnu[j], comp));
             }
+            double za0 = 0.0, za1 = 0.0;
+            if (live) {
 #pragma unroll
-            for (int s = 0; s < RB; ++s) {
-                if (!bon[s]) continue;
-                const double rp = bsign(bj[s]) * ((bj[s] < 2) ? du0 : du1) - sb[s] - bb[s];
-                rpmax = fmax(rpmax, fabs(rp));
-                comp = fma(sb[s], lb[s], comp);
-                if (bj[s] < 2) za0 += -bsign(bj[s]) * lb[s]; else za1 += -bsign(bj[s]) * lb[s];
-            }
-#pragma unroll
-            for (int a = 0; a < 4; ++a) ya[a] = stage_sum(ya[a]);
-            za0 = stage_sum(za0);
-            za1 = stage_sum(za1);
-            if (lead) {
+                for (int j = 0; j < NBOX; ++j) {
+                    const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
+                    rpmax = fmax(rpmax, fabs(rp));
+                    comp = fma(sb[j], lb[j], comp);
+                }
+                za0 = lb[1] - lb[0];
+                za1 = lb[3] - lb[2];
                 double Qs[10], qs[4], yc[4];
                 stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
@@ -728,96 +779,95 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 S.za[2 * (k - 1)] = za0;
                 S.za[2 * (k - 1) + 1] = za1;
             }
-            rpmax = G.max(rpmax);
-            rxmax = G.max(rxmax);
-            comp = G.sum(comp);
+            rpmax = Q.max(rpmax);
+            rxmax = Q.max(rxmax);
+            comp = Q.sum(comp);
             wave_sync();
-            double rdmax, sd;
-            dual_norms(S, N, dt, rdmax, sd);
+            PROF(2)
             mu = comp / Mtot;
-            if (!(mu == mu) || !(rdmax == rdmax)) { st_here = MPC_NUMERICAL; it = iter; done = true; break; }
+            if (!(mu == mu)) { st_here = MPC_NUMERICAL; it = iter; break; }
             if (mu <= Pr.tol_mu && rpmax <= 10.0 * Pr.tol * (1.0 + bscale) && rxmax <= Pr.tol * rho) {
                 // converged: the polish then makes the active set exact;
-                // the dual residual carries O(eps/mu) multiplier noise, required to 1e4*tol
+                // the dual residual carries O(eps/mu) multiplier noise, required to 1e4*tol.  Its
+                // adjoint recursion is only run here, once per solve.
+                double rdmax, sd;
+                dual_norms(S, N, dt, rdmax, sd);
+                PROF(3)
                 st_here = rdmax <= 1e4 * Pr.tol * (1.0 + sd) ? MPC_OK : MPC_NUMERICAL;
                 it = iter;
-                done = true;
                 break;
             }
             // -- barrier weights, augmented stage Hessians ---------------------------------------
-            double il[R], inu[R], wv[R], ilb[RB], wb[RB];
+            double il[NROW], inu[NROW], wv[NROW], ilb[NBOX], wb[NBOX];
             {
                 double Qp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                for (int s = 0; s < R; ++s) {
-                    il[s] = frcp(rl[s]);
-                    inu[s] = frcp(rnu[s]);
-                    wv[s] = ron[s] ? frcp(fma(rs[s], il[s], rxi[s] * inu[s])) : 0.0;   // 1/d
+                for (int j = 0; j < NROW; ++j) {
+                    il[j] = frcp(rl[j]);
+                    inu[j] = frcp(rnu[j]);
+                    wv[j] = ron[j] ? frcp(fma(rs[j], il[j], rxi[j] * inu[j])) : 0.0;   // 1/d
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
-                        for (int c = a; c < 4; ++c) Qp[p4(a, c)] = fma(wv[s] * cf[s][a], cf[s][c], Qp[p4(a, c)]);
-                }
-                double r0 = 0.0, r1 = 0.0;
-#pragma unroll
-                for (int s = 0; s < RB; ++s) {
-                    ilb[s] = frcp(lb[s]);
-                    wb[s] = bon[s] ? lb[s] * frcp(sb[s]) : 0.0;
-                    if (bj[s] < 2) r0 += wb[s]; else r1 += wb[s];
+                        for (int c = a; c < 4; ++c)
+                            if (cf[j][a] != 0.0 && cf[j][c] != 0.0)
+                                Qp[p4(a, c)] = fma(wv[j] * cf[j][a], cf[j][c], Qp[p4(a, c)]);
                 }
 #pragma unroll
-                for (int a = 0; a < 10; ++a) Qp[a] = stage_sum(Qp[a]);
-                r0 = stage_sum(r0);
-                r1 = stage_sum(r1);
-                if (lead) {
+                for (int j = 0; j < NBOX; ++j) {
+                    ilb[j] = frcp(lb[j]);
+                    wb[j] = live ? lb[j] * frcp(sb[j]) : 0.0;
+                }
+                if (live) {
                     double Qs[10], qs[4];
                     stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
                     for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a] + Qs[a];
-                    S.Rt[2 * (k - 1)] = R0 + r0;
-                    S.Rt[2 * (k - 1) + 1] = R1 + r1;
+                    S.Rt[2 * (k - 1)] = R0 + (wb[0] + wb[1]);
+                    S.Rt[2 * (k - 1) + 1] = R1 + (wb[2] + wb[3]);
                 }
             }
             wave_sync();
-            riccati_factor(S, G, N, dt, ln);
+            PROF(4)
+            riccati_factor(S, N, dt, gl);
+            PROF(5)
             // -- predictor, corrector (and, if needed, centred) solves ---------------------------------
-            double p4v[R], p5v[R], pbv[RB];
+            double p4v[NROW], p5v[NROW], pbv[NBOX];
+#pragma unroll
+            for (int j = 0; j < NROW; ++j) { p4v[j] = 0.0; p5v[j] = 0.0; }
+#pragma unroll
+            for (int j = 0; j < NBOX; ++j) pbv[j] = 0.0;
             double sig = 0.0;
-            bool applied = false;
 #pragma unroll 1
             for (int pass = 0; pass < 3; ++pass) {
                 // pass 0: affine predictor; 1: Mehrotra corrector; 2: plain centred direction, taken when
                 // the corrector would not reduce complementarity (oracle: comp_after > comp)
                 const double smu = (pass >= 1) ? sig * mu : 0.0;
-                double r4[R], r5[R], r4b[RB], rh[R], rhb[RB];
+                const double cw = (pass == 1) ? 1.0 : 0.0;     // weight of the second-order term
+                // reduced right-hand side per row, scaled by 1/d: wr = rh / d  (newton() of the oracle)
+                double wr[NROW], wrb[NBOX];
                 {
                     double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
-                    for (int s = 0; s < R; ++s) {
-                        r4[s] = rs[s] * rl[s] - smu;
-                        r5[s] = rxi[s] * rnu[s] - smu;
-                        if (pass == 1) { r4[s] += p4v[s]; r5[s] += p5v[s]; }
-                        const double rp = dot4(cf[s], x4) + rxi[s] - rs[s] - bk[s];
-                        const double rx = rho - rl[s] - rnu[s];
-                        rh[s] = -rp - r4[s] * il[s] + fma(rxi[s], rx, r5[s]) * inu[s];
-                        const double w = ron[s] ? rh[s] * wv[s] : 0.0;
+                    for (int j = 0; j < NROW; ++j) {
+                        const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
+                        const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
+                        const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
+                        const double rx = rho - rl[j] - rnu[j];
+                        const double rh = -rp - r4 * il[j] + fma(rxi[j], rx, r5) * inu[j];
+                        wr[j] = ron[j] ? rh * wv[j] : 0.0;
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) q4[a] = fma(cf[s][a], w, q4[a]);
+                        for (int a = 0; a < 4; ++a)
+                            if (cf[j][a] != 0.0) q4[a] = fma(cf[j][a], wr[j], q4[a]);
                     }
 #pragma unroll
-                    for (int s = 0; s < RB; ++s) {
-                        r4b[s] = sb[s] * lb[s] - smu;
-                        if (pass == 1) r4b[s] += pbv[s];
-                        const double rp = bsign(bj[s]) * ((bj[s] < 2) ? du0 : du1) - sb[s] - bb[s];
-                        rhb[s] = -rp - r4b[s] * ilb[s];
-                        const double v = bsign(bj[s]) * rhb[s] * wb[s];
-                        if (bj[s] < 2) g0 += v; else g1 += v;
+                    for (int j = 0; j < NBOX; ++j) {
+                        const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
+                        const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
+                        wrb[j] = (-rp - r4 * ilb[j]) * wb[j];
+                        if (j < 2) g0 += bsign(j) * wrb[j]; else g1 += bsign(j) * wrb[j];
                     }
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) q4[a] = stage_sum(q4[a]);
-                    g0 = stage_sum(g0);
-                    g1 = stage_sum(g1);
-                    if (lead) {
+                    if (live) {
 #pragma unroll
                         for (int a = 0; a < 4; ++a) S.qh[4 * k + a] = q4[a] - (S.yc[4 * k + a] + S.ya[4 * k + a]);
                         S.gh[2 * (k - 1)] = g0 - (S.zc[2 * (k - 1)] + S.za[2 * (k - 1)]);
@@ -825,311 +875,304 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     }
                 }
                 wave_sync();
-                riccati_solve(S, N, dt, ln);
-                // row directions and the step length
-                double dsv[R], dlv[R], dxv[R], dnv[R], dsb[RB], dlb[RB];
+                PROF(6)
+                riccati_solve(S, N, dt, gl);
+                PROF(7)
+                // row directions and the largest feasible step
+                double dx4[4];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
+                const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
+                double dsv[NROW], dlv[NROW], dxv[NROW], dnv[NROW], dsb[NBOX], dlb[NBOX];
                 double amax = 1.0;
-                {
-                    double dx4[4];
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
-#pragma unroll
-                    for (int s = 0; s < R; ++s) {
-                        const double rx = rho - rl[s] - rnu[s];
-                        const double dl = (rh[s] - dot4(cf[s], dx4)) * wv[s];
-                        const double ds = -fma(rs[s], dl, r4[s]) * il[s];
-                        const double dn = rx - dl;
-                        const double dxi = -fma(rxi[s], dn, r5[s]) * inu[s];
-                        dsv[s] = ds; dlv[s] = dl; dxv[s] = dxi; dnv[s] = dn;
-                        if (!ron[s]) continue;
-                        if (ds < 0.0) amax = fmin(amax, -rs[s] / ds);
-                        if (dl < 0.0) amax = fmin(amax, -rl[s] / dl);
-                        if (dxi < 0.0) amax = fmin(amax, -rxi[s] / dxi);
-                        if (dn < 0.0) amax = fmin(amax, -rnu[s] / dn);
-                    }
-                    const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
-#pragma unroll
-                    for (int s = 0; s < RB; ++s) {
-                        const double duu = (bj[s] < 2) ? dd0 : dd1;
-                        const double dl = (rhb[s] - bsign(bj[s]) * duu) * wb[s];
-                        const double ds = -fma(sb[s], dl, r4b[s]) * ilb[s];
-                        dsb[s] = ds; dlb[s] = dl;
-                        if (!bon[s]) continue;
-                        if (ds < 0.0) amax = fmin(amax, -sb[s] / ds);
-                        if (dl < 0.0) amax = fmin(amax, -lb[s] / dl);
-                    }
+                for (int j = 0; j < NROW; ++j) {
+                    const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
+                    const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
+                    const double rx = rho - rl[j] - rnu[j];
+                    const double dl = fma(-wv[j], dot4(cf[j], dx4), wr[j]);
+                    const double ds = -fma(rs[j], dl, r4) * il[j];
+                    const double dn = rx - dl;
+                    const double dxi = -fma(rxi[j], dn, r5) * inu[j];
+                    const bool on = ron[j];
+                    dsv[j] = on ? ds : 0.0;
+                    dlv[j] = on ? dl : 0.0;
+                    dxv[j] = on ? dxi : 0.0;
+                    dnv[j] = on ? dn : 0.0;
+                    // ratio tests: the approximate reciprocal is enough for a step length
+                    if (dsv[j] < 0.0) amax = fmin(amax, -rs[j] * __builtin_amdgcn_rcp(dsv[j]));
+                    if (dlv[j] < 0.0) amax = fmin(amax, -rl[j] * __builtin_amdgcn_rcp(dlv[j]));
+                    if (dxv[j] < 0.0) amax = fmin(amax, -rxi[j] * __builtin_amdgcn_rcp(dxv[j]));
+                    if (dnv[j] < 0.0) amax = fmin(amax, -rnu[j] * __builtin_amdgcn_rcp(dnv[j]));
                 }
-                amax = G.min(amax);
+#pragma unroll
+                for (int j = 0; j < NBOX; ++j) {
+                    const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
+                    const double dl = fma(-wb[j] * bsign(j), (j < 2 ? dd0 : dd1), wrb[j]);
+                    const double ds = -fma(sb[j], dl, r4) * ilb[j];
+                    dsb[j] = live ? ds : 0.0;
+                    dlb[j] = live ? dl : 0.0;
+                    if (dsb[j] < 0.0) amax = fmin(amax, -sb[j] * __builtin_amdgcn_rcp(dsb[j]));
+                    if (dlb[j] < 0.0) amax = fmin(amax, -lb[j] * __builtin_amdgcn_rcp(dlb[j]));
+                }
+                amax = Q.min(amax);
                 // complementarity after the step (pass 0: at the full affine step length)
                 const double a_try = (pass == 0) ? amax : fmin(1.0, TAU * amax);
                 double ca = 0.0;
 #pragma unroll
-                for (int s = 0; s < R; ++s)
-                    if (ron[s])
-                        ca += fma(a_try, dsv[s], rs[s]) * fma(a_try, dlv[s], rl[s]) +
-                              fma(a_try, dxv[s], rxi[s]) * fma(a_try, dnv[s], rnu[s]);
+                for (int j = 0; j < NROW; ++j)
+                    if (ron[j])
+                        ca += fma(a_try, dsv[j], rs[j]) * fma(a_try, dlv[j], rl[j]) +
+                              fma(a_try, dxv[j], rxi[j]) * fma(a_try, dnv[j], rnu[j]);
+                if (live) {
 #pragma unroll
-                for (int s = 0; s < RB; ++s)
-                    if (bon[s]) ca += fma(a_try, dsb[s], sb[s]) * fma(a_try, dlb[s], lb[s]);
-                ca = G.sum(ca);
+                    for (int j = 0; j < NBOX; ++j) ca += fma(a_try, dsb[j], sb[j]) * fma(a_try, dlb[j], lb[j]);
+                }
+                ca = Q.sum(ca);
                 if (pass == 0) {
                     const double r = ca / comp;
                     sig = r * r * r;
 #pragma unroll
-                    for (int s = 0; s < R; ++s) { p4v[s] = dsv[s] * dlv[s]; p5v[s] = dxv[s] * dnv[s]; }
+                    for (int j = 0; j < NROW; ++j) { p4v[j] = dsv[j] * dlv[j]; p5v[j] = dxv[j] * dnv[j]; }
 #pragma unroll
-                    for (int s = 0; s < RB; ++s) pbv[s] = dsb[s] * dlb[s];
+                    for (int j = 0; j < NBOX; ++j) pbv[j] = dsb[j] * dlb[j];
                     continue;
                 }
                 if (pass == 1 && ca > comp) continue;     // safeguard: take the centred direction
                 const double alpha = a_try;
-                applied = true;
                 stall = (mu < 1e-6 && ca > 0.9 * comp) ? stall + 1 : 0;
 #pragma unroll
-                for (int s = 0; s < R; ++s) {
-                    if (!ron[s]) continue;
-                    rs[s] = fma(alpha, dsv[s], rs[s]);
-                    rl[s] = fma(alpha, dlv[s], rl[s]);
-                    rxi[s] = fma(alpha, dxv[s], rxi[s]);
-                    rnu[s] = fma(alpha, dnv[s], rnu[s]);
+                for (int j = 0; j < NROW; ++j) {
+                    rs[j] = fma(alpha, dsv[j], rs[j]);
+                    rl[j] = fma(alpha, dlv[j], rl[j]);
+                    rxi[j] = fma(alpha, dxv[j], rxi[j]);
+                    rnu[j] = fma(alpha, dnv[j], rnu[j]);
                 }
 #pragma unroll
-                for (int s = 0; s < RB; ++s) {
-                    if (!bon[s]) continue;
-                    sb[s] = fma(alpha, dsb[s], sb[s]);
-                    lb[s] = fma(alpha, dlb[s], lb[s]);
+                for (int j = 0; j < NBOX; ++j) {
+                    sb[j] = fma(alpha, dsb[j], sb[j]);
+                    lb[j] = fma(alpha, dlb[j], lb[j]);
                 }
-                if (ln < N) {
-                    S.du[2 * ln] = fma(alpha, S.dud[2 * ln], S.du[2 * ln]);
-                    S.du[2 * ln + 1] = fma(alpha, S.dud[2 * ln + 1], S.du[2 * ln + 1]);
-                }
+                du0 = fma(alpha, dd0, du0);
+                du1 = fma(alpha, dd1, du1);
+#pragma unroll
+                for (int a = 0; a < 4; ++a) x4[a] = fma(alpha, dx4[a], x4[a]);
                 break;
             }
-            (void)applied;
             wave_sync();
+            PROF(8)
             it = iter + 1;
-            if (stall >= 5) { st_here = MPC_NUMERICAL; done = true; break; }
+            if (stall >= 5) { st_here = MPC_NUMERICAL; break; }
         }
-        (void)done;
         total_it += it;
         // NaN guard and the infeasibility flag
         double bad = 0.0;
-        if (ln < N) bad = (S.du[2 * ln] == S.du[2 * ln] && S.du[2 * ln + 1] == S.du[2 * ln + 1]) ? 0.0 : 1.0;
-        bad = G.max(bad);
+        if (live) bad = (du0 == du0 && du1 == du1) ? 0.0 : 1.0;
+        bad = Q.max(bad);
         if (bad > 0.0) {
             st_here = MPC_NUMERICAL;
-            if (ln < N) { S.du[2 * ln] = 0.0; S.du[2 * ln + 1] = 0.0; }
+            du0 = 0.0;
+            du1 = 0.0;
         } else if (st_here == MPC_OK) {
             double inf = 0.0;
 #pragma unroll
-            for (int s = 0; s < R; ++s)
-                if (ron[s] && rxi[s] > 1e-6 * (1.0 + fabs(bk[s]))) inf = 1.0;
-            if (G.max(inf) > 0.0) st_here = MPC_INFEASIBLE;
+            for (int j = 0; j < NROW; ++j)
+                if (ron[j] && rxi[j] > 1e-6 * (1.0 + fabs(bk[j]))) inf = 1.0;
+            if (Q.max(inf) > 0.0) st_here = MPC_INFEASIBLE;
         }
         wave_sync();
 
         // ---- active-set polish (oracle polish()) --------------------------
+        PROF(8)
         if (Pr.polish && bad == 0.0) {
             // class per row: 0 inactive, 1 active (equality), 2 violated (multiplier fixed at rho)
-            int cls[R], clb[RB];
+            int cls[NROW], clb[NBOX];
 #pragma unroll
-            for (int s = 0; s < R; ++s) cls[s] = !ron[s] ? 0 : (rxi[s] > rnu[s] ? 2 : (rl[s] > rs[s] ? 1 : 0));
+            for (int j = 0; j < NROW; ++j) cls[j] = !ron[j] ? 0 : (rxi[j] > rnu[j] ? 2 : (rl[j] > rs[j] ? 1 : 0));
 #pragma unroll
-            for (int s = 0; s < RB; ++s) clb[s] = (bon[s] && lb[s] > sb[s]) ? 1 : 0;
-            if (ln < N) { S.dub[2 * ln] = S.du[2 * ln]; S.dub[2 * ln + 1] = S.du[2 * ln + 1]; }
-            wave_sync();
+            for (int j = 0; j < NBOX; ++j) clb[j] = (live && lb[j] > sb[j]) ? 1 : 0;
+            // the interior-point iterate (du, x4) is the start of every round and the fallback
+            double pu0 = du0, pu1 = du1;
             bool accepted = false;
             double nviol_acc = 0.0;
             for (int round = 0; round < POLISH_ROUNDS; ++round) {
-                double tl[R], tlb[RB];
-                {
-                    if (ln < N) { S.du[2 * ln] = S.dub[2 * ln]; S.du[2 * ln + 1] = S.dub[2 * ln + 1]; }
+                double tl[NROW], tlb[NBOX];
+#pragma unroll
+                for (int j = 0; j < NROW; ++j) tl[j] = rl[j];
+#pragma unroll
+                for (int j = 0; j < NBOX; ++j) tlb[j] = lb[j];
+                if (live) {
                     double Qp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                    for (int s = 0; s < R; ++s) {
-                        tl[s] = rl[s];
-                        const double w = cls[s] == 1 ? 1.0 / POLISH_DELTA : 0.0;
+                    for (int j = 0; j < NROW; ++j) {
+                        const double w = cls[j] == 1 ? 1.0 / POLISH_DELTA : 0.0;
 #pragma unroll
                         for (int a = 0; a < 4; ++a)
 #pragma unroll
-                            for (int c = a; c < 4; ++c) Qp[p4(a, c)] = fma(w * cf[s][a], cf[s][c], Qp[p4(a, c)]);
+                            for (int c = a; c < 4; ++c)
+                                if (cf[j][a] != 0.0 && cf[j][c] != 0.0)
+                                    Qp[p4(a, c)] = fma(w * cf[j][a], cf[j][c], Qp[p4(a, c)]);
                     }
-                    double r0 = 0.0, r1 = 0.0;
+                    double Qs[10], qs[4];
+                    stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
-                    for (int s = 0; s < RB; ++s) {
-                        tlb[s] = lb[s];
-                        if (clb[s] == 1) { if (bj[s] < 2) r0 += 1.0 / POLISH_DELTA; else r1 += 1.0 / POLISH_DELTA; }
-                    }
+                    for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a] + Qs[a];
+                    S.Rt[2 * (k - 1)] = R0 + (clb[0] + clb[1]) * (1.0 / POLISH_DELTA);
+                    S.Rt[2 * (k - 1) + 1] = R1 + (clb[2] + clb[3]) * (1.0 / POLISH_DELTA);
+                }
+                wave_sync();
+                riccati_factor(S, N, dt, gl);
+                double xp[4] = {x4[0], x4[1], x4[2], x4[3]};
+                pu0 = du0;
+                pu1 = du1;
+#pragma unroll 1
+                for (int r = 0; r < POLISH_REFINE; ++r) {
+                    // exact KKT residual of the equality QP -> LQR right-hand side
+                    double r2[NROW], r2b[NBOX];
 #pragma unroll
-                    for (int a = 0; a < 10; ++a) Qp[a] = stage_sum(Qp[a]);
-                    r0 = stage_sum(r0);
-                    r1 = stage_sum(r1);
-                    if (lead) {
+                    for (int j = 0; j < NROW; ++j) r2[j] = (cls[j] == 1) ? bk[j] - dot4(cf[j], xp) : 0.0;
+#pragma unroll
+                    for (int j = 0; j < NBOX; ++j) r2b[j] = (clb[j] == 1) ? bb[j] - bsign(j) * (j < 2 ? pu0 : pu1) : 0.0;
+                    if (live) {
+                        double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
+#pragma unroll
+                        for (int j = 0; j < NROW; ++j) {
+                            const double wgt = (cls[j] == 2) ? rho : (cls[j] == 1 ? tl[j] + r2[j] * (1.0 / POLISH_DELTA) : 0.0);
+#pragma unroll
+                            for (int a = 0; a < 4; ++a)
+                                if (cf[j][a] != 0.0) q4[a] = fma(cf[j][a], wgt, q4[a]);
+                        }
+#pragma unroll
+                        for (int j = 0; j < NBOX; ++j) {
+                            const double v = (clb[j] == 1) ? bsign(j) * (tlb[j] + r2b[j] * (1.0 / POLISH_DELTA)) : 0.0;
+                            if (j < 2) g0 += v; else g1 += v;
+                        }
                         double Qs[10], qs[4];
                         stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
-                        for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a] + Qs[a];
-                        S.Rt[2 * (k - 1)] = R0 + r0;
-                        S.Rt[2 * (k - 1) + 1] = R1 + r1;
-                    }
-                }
-                wave_sync();
-                riccati_factor(S, G, N, dt, ln);
-                double x4[4];
-#pragma unroll 1
-                for (int r = 0; r <= POLISH_REFINE; ++r) {
-                    rollout_lin(S, N, dt, S.du, S.dX, ln);
+                        for (int a = 0; a < 4; ++a) {
+                            double acc = qs[a];
 #pragma unroll
-                    for (int a = 0; a < 4; ++a) x4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
-                    if (r == POLISH_REFINE) break;
-                    // exact KKT residual of the equality QP -> LQR right-hand side
-                    double r2[R], r2b[RB];
-                    const double du0 = live ? S.du[2 * (k - 1)] : 0.0, du1 = live ? S.du[2 * (k - 1) + 1] : 0.0;
-                    {
-                        double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
-#pragma unroll
-                        for (int s = 0; s < R; ++s) {
-                            r2[s] = (cls[s] == 1) ? bk[s] - dot4(cf[s], x4) : 0.0;
-                            const double wgt = (cls[s] == 2) ? rho : (cls[s] == 1 ? tl[s] + r2[s] * (1.0 / POLISH_DELTA) : 0.0);
-#pragma unroll
-                            for (int a = 0; a < 4; ++a) q4[a] = fma(cf[s][a], wgt, q4[a]);
+                            for (int c = 0; c < 4; ++c) acc = fma(Qs[p4(a, c)], xp[c], acc);
+                            S.qh[4 * k + a] = q4[a] - acc;
                         }
-#pragma unroll
-                        for (int s = 0; s < RB; ++s) {
-                            const double uu = (bj[s] < 2) ? du0 : du1;
-                            r2b[s] = (clb[s] == 1) ? bb[s] - bsign(bj[s]) * uu : 0.0;
-                            const double v = (clb[s] == 1) ? bsign(bj[s]) * (tlb[s] + r2b[s] * (1.0 / POLISH_DELTA)) : 0.0;
-                            if (bj[s] < 2) g0 += v; else g1 += v;
-                        }
-#pragma unroll
-                        for (int a = 0; a < 4; ++a) q4[a] = stage_sum(q4[a]);
-                        g0 = stage_sum(g0);
-                        g1 = stage_sum(g1);
-                        if (lead) {
-                            double Qs[10], qs[4];
-                            stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
-#pragma unroll
-                            for (int a = 0; a < 4; ++a) {
-                                double acc = qs[a];
-#pragma unroll
-                                for (int c = 0; c < 4; ++c) acc = fma(Qs[p4(a, c)], x4[c], acc);
-                                S.qh[4 * k + a] = q4[a] - acc;
-                            }
-                            S.gh[2 * (k - 1)] = g0 - fma(R0, du0, R0 * S.ub[2 * (k - 1)]);
-                            S.gh[2 * (k - 1) + 1] = g1 - fma(R1, du1, R1 * S.ub[2 * (k - 1) + 1]);
-                        }
+                        S.gh[2 * (k - 1)] = g0 - fma(R0, pu0, R0 * S.ub[2 * (k - 1)]);
+                        S.gh[2 * (k - 1) + 1] = g1 - fma(R1, pu1, R1 * S.ub[2 * (k - 1) + 1]);
                     }
                     wave_sync();
-                    riccati_solve(S, N, dt, ln);
+                    riccati_solve(S, N, dt, gl);
                     {
                         double dx4[4];
 #pragma unroll
                         for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
 #pragma unroll
-                        for (int s = 0; s < R; ++s)
-                            if (cls[s] == 1) tl[s] += (r2[s] - dot4(cf[s], dx4)) * (1.0 / POLISH_DELTA);
+                        for (int j = 0; j < NROW; ++j)
+                            if (cls[j] == 1) tl[j] += (r2[j] - dot4(cf[j], dx4)) * (1.0 / POLISH_DELTA);
                         const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
 #pragma unroll
-                        for (int s = 0; s < RB; ++s)
-                            if (clb[s] == 1)
-                                tlb[s] += (r2b[s] - bsign(bj[s]) * ((bj[s] < 2) ? dd0 : dd1)) * (1.0 / POLISH_DELTA);
+                        for (int j = 0; j < NBOX; ++j)
+                            if (clb[j] == 1) tlb[j] += (r2b[j] - bsign(j) * (j < 2 ? dd0 : dd1)) * (1.0 / POLISH_DELTA);
+#pragma unroll
+                        for (int a = 0; a < 4; ++a) xp[a] += dx4[a];
+                        pu0 += dd0;
+                        pu1 += dd1;
                     }
-                    wave_sync();
-                    if (ln < N) { S.du[2 * ln] += S.dud[2 * ln]; S.du[2 * ln + 1] += S.dud[2 * ln + 1]; }
                     wave_sync();
                 }
                 // acceptance: KKT consistency; otherwise flip every offending row and retry
                 double lmax = 1.0;
 #pragma unroll
-                for (int s = 0; s < R; ++s)
-                    if (cls[s] == 1) lmax = fmax(lmax, fabs(tl[s]));
+                for (int j = 0; j < NROW; ++j)
+                    if (cls[j] == 1) lmax = fmax(lmax, fabs(tl[j]));
 #pragma unroll
-                for (int s = 0; s < RB; ++s)
-                    if (clb[s] == 1) lmax = fmax(lmax, fabs(tlb[s]));
-                lmax = G.max(lmax);
+                for (int j = 0; j < NBOX; ++j)
+                    if (clb[j] == 1) lmax = fmax(lmax, fabs(tlb[j]));
+                lmax = Q.max(lmax);
                 double worst = 0.0, nviol = 0.0, finite = 1.0;
-                bool flip[R], flipb[RB];
-                {
-                    const double du0 = live ? S.du[2 * (k - 1)] : 0.0, du1 = live ? S.du[2 * (k - 1) + 1] : 0.0;
-                    if (!(du0 == du0) || !(du1 == du1)) finite = 0.0;
+                bool flip[NROW], flipb[NBOX];
+                if (live && (!(pu0 == pu0) || !(pu1 == pu1))) finite = 0.0;
 #pragma unroll
-                    for (int s = 0; s < R; ++s) {
-                        flip[s] = false;
-                        if (!ron[s]) continue;
-                        const double bsc = 1.0 + fabs(bk[s]);
-                        const double r = dot4(cf[s], x4) - bk[s];
-                        double badv = 0.0;
-                        if (cls[s] == 1) {
-                            if (tl[s] < -1e-9 * lmax) badv = -tl[s] / lmax;
-                            else if (tl[s] > rho * (1.0 + 1e-9)) badv = (tl[s] - rho) / lmax;
-                            else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
-                        } else if (cls[s] == 2) {
-                            if (r > 1e-9 * bsc) badv = r / bsc;
-                            if (r < -1e-6 * bsc) nviol += 1.0;
-                        } else if (r < -1e-9 * bsc) badv = -r / bsc;
-                        worst = fmax(worst, badv);
-                        flip[s] = badv > 0.0;
-                    }
-#pragma unroll
-                    for (int s = 0; s < RB; ++s) {
-                        flipb[s] = false;
-                        if (!bon[s]) continue;
-                        const double bsc = 1.0 + fabs(bb[s]);
-                        const double r = bsign(bj[s]) * ((bj[s] < 2) ? du0 : du1) - bb[s];
-                        double badv = 0.0;
-                        if (clb[s] == 1) {
-                            if (tlb[s] < -1e-9 * lmax) badv = -tlb[s] / lmax;
-                            else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
-                        } else if (r < -1e-9 * bsc) badv = -r / bsc;
-                        worst = fmax(worst, badv);
-                        flipb[s] = badv > 0.0;
-                    }
+                for (int j = 0; j < NROW; ++j) {
+                    flip[j] = false;
+                    if (!ron[j]) continue;
+                    const double bsc = 1.0 + fabs(bk[j]);
+                    const double r = dot4(cf[j], xp) - bk[j];
+                    double badv = 0.0;
+                    if (cls[j] == 1) {
+                        if (tl[j] < -1e-9 * lmax) badv = -tl[j] / lmax;
+                        else if (tl[j] > rho * (1.0 + 1e-9)) badv = (tl[j] - rho) / lmax;
+                        else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
+                    } else if (cls[j] == 2) {
+                        if (r > 1e-9 * bsc) badv = r / bsc;
+                        if (r < -1e-6 * bsc) nviol += 1.0;
+                    } else if (r < -1e-9 * bsc) badv = -r / bsc;
+                    worst = fmax(worst, badv);
+                    flip[j] = badv > 0.0;
                 }
-                worst = G.max(worst);
-                nviol = G.sum(nviol);
-                finite = G.min(finite);
+#pragma unroll
+                for (int j = 0; j < NBOX; ++j) {
+                    flipb[j] = false;
+                    if (!live) continue;
+                    const double bsc = 1.0 + fabs(bb[j]);
+                    const double r = bsign(j) * (j < 2 ? pu0 : pu1) - bb[j];
+                    double badv = 0.0;
+                    if (clb[j] == 1) {
+                        if (tlb[j] < -1e-9 * lmax) badv = -tlb[j] / lmax;
+                        else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
+                    } else if (r < -1e-9 * bsc) badv = -r / bsc;
+                    worst = fmax(worst, badv);
+                    flipb[j] = badv > 0.0;
+                }
+                worst = Q.max(worst);
+                nviol = Q.sum(nviol);
+                finite = Q.min(finite);
                 if (finite == 0.0) break;
                 if (worst == 0.0) {
                     accepted = true;
                     nviol_acc = nviol;
-                    if (ln < N) { S.dub[2 * ln] = S.du[2 * ln]; S.dub[2 * ln + 1] = S.du[2 * ln + 1]; }
-                    wave_sync();
                     break;
                 }
 #pragma unroll
-                for (int s = 0; s < R; ++s)
-                    if (flip[s]) cls[s] = (cls[s] == 1) ? (tl[s] > rho ? 2 : 0) : 1;
+                for (int j = 0; j < NROW; ++j)
+                    if (flip[j]) cls[j] = (cls[j] == 1) ? (tl[j] > rho ? 2 : 0) : 1;
 #pragma unroll
-                for (int s = 0; s < RB; ++s)
-                    if (flipb[s]) clb[s] = 1 - clb[s];
+                for (int j = 0; j < NBOX; ++j)
+                    if (flipb[j]) clb[j] = 1 - clb[j];
                 wave_sync();
             }
-            // the accepted polish (or, if none, the interior-point iterate) is in dub
-            if (ln < N) { S.du[2 * ln] = S.dub[2 * ln]; S.du[2 * ln + 1] = S.dub[2 * ln + 1]; }
-            if (accepted) st_here = nviol_acc > 0.0 ? MPC_INFEASIBLE : MPC_OK;
+            if (accepted) {
+                du0 = pu0;
+                du1 = pu1;
+                st_here = nviol_acc > 0.0 ? MPC_INFEASIBLE : MPC_OK;
+            }
             wave_sync();
         }
         status = st_here;
-        if (ln < N) {
-            S.ub[2 * ln] += S.du[2 * ln];
-            S.ub[2 * ln + 1] += S.du[2 * ln + 1];
+        if (live) {
+            S.ub[2 * (k - 1)] += du0;
+            S.ub[2 * (k - 1) + 1] += du1;
         }
         wave_sync();
     }
 
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------
-    predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, ln);
-    if (ln < N && Ug) {
-        Ug[(size_t)b * 2 * N + 2 * ln] = S.ub[2 * ln];
-        Ug[(size_t)b * 2 * N + 2 * ln + 1] = S.ub[2 * ln + 1];
+    PROF(9)
+    predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
+    if (bvalid) {
+        if (gl < N && Ug) {
+            Ug[(size_t)b * 2 * N + 2 * gl] = S.ub[2 * gl];
+            Ug[(size_t)b * 2 * N + 2 * gl + 1] = S.ub[2 * gl + 1];
+        }
+        if (Xg)
+            for (int i = gl; i < 5 * NP; i += GL) Xg[(size_t)b * 5 * NP + i] = S.Xr[i];
+        if (gl == 0) {
+            if (u0g) { u0g[2 * (size_t)b] = S.ub[0]; u0g[2 * (size_t)b + 1] = S.ub[1]; }
+            if (statusg) statusg[b] = status;
+            if (itersg) itersg[b] = total_it;
+        }
     }
-    if (Xg)
-        for (int i = ln; i < 5 * NP; i += WAVE) Xg[(size_t)b * 5 * NP + i] = S.Xr[i];
-    if (ln == 0) {
-        if (u0g) { u0g[2 * (size_t)b] = S.ub[0]; u0g[2 * (size_t)b + 1] = S.ub[1]; }
-        if (statusg) statusg[b] = status;
-        if (itersg) itersg[b] = total_it;
-    }
+    PROF(10)
+    PROF_END
 }
 
 __global__ void mpc_lookup_kernel(DevTable tab, int n, const double* __restrict__ s, double* __restrict__ st,
@@ -1201,6 +1244,18 @@ extern "C" void mpc_default_params(mpc_params* p) {
 }
 
 extern "C" const char* mpc_last_error(void) { return g_err.c_str(); }
+
+#ifdef MPC_PROF
+// diagnostic build only: accumulated shader cycles per kernel phase (lane 0 of every instance)
+extern "C" int mpc_debug_prof(unsigned long long* out, int reset) {
+    if (out) HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16), MPC_E_DEVICE);
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)), MPC_E_DEVICE);
+    }
+    return MPC_SUCCESS;
+}
+#endif
 extern "C" int mpc_version(void) { return MPCQP_VERSION; }
 
 static int check_params(const mpc_params* p) {
@@ -1344,18 +1399,22 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
     size_t lds = sizeof(double) * (size_t)lds_doubles(kp.N);
     if (lds > 160 * 1024) return fail(MPC_E_ARG, "horizon too long for LDS");
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
-    // rows of a stage spread over P lanes: all 64 lanes carry row state when N is short
+    // G = 64 / GL instances per wavefront: the smallest lane group holding the N + 1 stages
     const int* nob = obs ? n_obs : nullptr;
     hipStream_t st = (hipStream_t)stream;
-    if (3 * kp.N <= WAVE)
-        hipLaunchKernelGGL(mpc_solve_kernel<3>, dim3(B), dim3(WAVE), lds, st, c->tab, kp, B, x0, obs, nob, ubar, u0,
-                           U, Xpred, status, iters);
-    else if (2 * kp.N <= WAVE)
-        hipLaunchKernelGGL(mpc_solve_kernel<2>, dim3(B), dim3(WAVE), lds, st, c->tab, kp, B, x0, obs, nob, ubar, u0,
-                           U, Xpred, status, iters);
+    const int GL = kp.N + 1 <= 16 ? 16 : (kp.N + 1 <= 32 ? 32 : 64);
+    const int G = WAVE / GL;
+    const size_t lds_wave = lds * G;
+    const dim3 grid((B + G - 1) / G);
+    if (GL == 16)
+        hipLaunchKernelGGL(mpc_solve_kernel<16>, grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, ubar,
+                           u0, U, Xpred, status, iters);
+    else if (GL == 32)
+        hipLaunchKernelGGL(mpc_solve_kernel<32>, grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, ubar,
+                           u0, U, Xpred, status, iters);
     else
-        hipLaunchKernelGGL(mpc_solve_kernel<1>, dim3(B), dim3(WAVE), lds, st, c->tab, kp, B, x0, obs, nob, ubar, u0,
-                           U, Xpred, status, iters);
+        hipLaunchKernelGGL(mpc_solve_kernel<64>, grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, ubar,
+                           u0, U, Xpred, status, iters);
     HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
     return MPC_SUCCESS;
 }

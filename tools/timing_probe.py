@@ -9,6 +9,8 @@ import torch
 import __graft_entry__ as ge
 ge.build()
 import mpcqp
+if os.environ.get("PROBE_LIB"):          # time an alternative in-tree build of the same ABI
+    mpcqp.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", os.environ["PROBE_LIB"])
 import workloads as W
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
