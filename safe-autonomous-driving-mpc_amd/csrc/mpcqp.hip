@@ -573,13 +573,18 @@ __device__ unsigned long long g_prof[16];
 // the inherently sequential part of the algorithm on a 64-wide SIMD.
 // All branching is group-uniform, so a group that has converged simply drops out of the exec mask.
 // ------------------------------------------------------------------------------------------
-template <int GL>
+// soft-row id of lane slot j: without obstacles the slots hold rows 0-5 and 8
+template <bool OBS>
+__device__ __forceinline__ constexpr int rid(int j) { return OBS ? j : (j < 6 ? j : 8); }
+
+template <int GL, bool OBS>
 __global__ void __launch_bounds__(WAVE)
 mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g, const double* __restrict__ obsg,
                  const int* __restrict__ nobsg, const double* __restrict__ ubarg, double* __restrict__ u0g,
                  double* __restrict__ Ug, double* __restrict__ Xg, int* __restrict__ statusg,
                  int* __restrict__ itersg) {
     constexpr int G = WAVE / GL;
+    constexpr int NR = OBS ? NROW : NROW - 2;    // soft rows held per lane (6, 7: obstacle rows)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int ln = threadIdx.x;
     const int grp = ln / GL, gl = ln % GL;
@@ -605,12 +610,12 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 
     const int k = gl + 1;            // stage of this lane
     const bool live = k <= N;        // lane owns the rows of stage k and the boxes of control k-1
-    bool ron[NROW];
-    double cf[NROW][4];
+    bool ron[NR];
+    double cf[NR][4];
 #pragma unroll
-    for (int j = 0; j < NROW; ++j) {
-        ron[j] = live && ((j != 6 && j != 7) || has_obs);
-        row_coef(j, hL, Pr.L, Pr.tgap, cf[j]);
+    for (int j = 0; j < NR; ++j) {
+        ron[j] = live && ((rid<OBS>(j) != 6 && rid<OBS>(j) != 7) || has_obs);
+        row_coef(rid<OBS>(j), hL, Pr.L, Pr.tgap, cf[j]);
     }
 
     // ---- K1: linearisation point ---------------------------------------------------------
@@ -637,7 +642,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     wave_sync();
 
     int nsoft = 0;
-    for (int j = 0; j < NROW; ++j) nsoft += ((j != 6 && j != 7) || has_obs) ? 1 : 0;
+    for (int jj = 0; jj < NROW; ++jj) nsoft += ((jj != 6 && jj != 7) || has_obs) ? 1 : 0;
     const double Mtot = (double)(2 * nsoft * N + NBOX * N);
     const double R0 = 2.0 * Pr.w_u1, R1 = 2.0 * Pr.w_u2;
 
@@ -675,7 +680,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             }
         }
         // row bounds of stage k, box bounds of control k-1
-        double bk[NROW], bb[NBOX];
+        double bk[NR], bb[NBOX];
         double bscale_l = 0.0;
         {
             double shat = INFINITY;
@@ -687,7 +692,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             const double* x = S.Xr + 5 * (live ? k : 0);
             const double sl = Pr.sl;
             const double pv0 = x[1], pv1 = x[1] + hL * x[2], pv2 = x[1] + Pr.L * x[2];
-            double v[NROW];
+            double v[NROW];  // by row id
             v[0] = -sl - pv0;
             v[1] = -(sl - pv0);
             v[2] = -sl - pv1;
@@ -698,8 +703,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             v[7] = has_obs ? -(shat - x[0] - Pr.tgap * x[4]) : 0.0;
             v[8] = -x[4];
 #pragma unroll
-            for (int j = 0; j < NROW; ++j) {
-                bk[j] = ron[j] ? v[j] : 0.0;
+            for (int j = 0; j < NR; ++j) {
+                bk[j] = ron[j] ? v[rid<OBS>(j)] : 0.0;
                 bscale_l = fmax(bscale_l, fabs(bk[j]));
             }
             const double ub0 = live ? S.ub[2 * (k - 1)] : 0.0, ub1 = live ? S.ub[2 * (k - 1) + 1] : 0.0;
@@ -714,9 +719,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         wave_sync();
 
         // ---- K4: PDIP; interior-point state of this lane's rows in registers ---------------------
-        double rs[NROW], rl[NROW], rxi[NROW], rnu[NROW], sb[NBOX], lb[NBOX];
+        double rs[NR], rl[NR], rxi[NR], rnu[NR], sb[NBOX], lb[NBOX];
 #pragma unroll
-        for (int j = 0; j < NROW; ++j) {
+        for (int j = 0; j < NR; ++j) {
             // centred start: xi covers the violation, s*lam = MU0 with lam <= rho/2, nu = rho - lam
             const double r0 = -bk[j];
             const double xi = (r0 < 0 ? -r0 : 0.0) + XI0;
@@ -743,7 +748,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             double rpmax = 0.0, rxmax = 0.0, comp = 0.0;
             double ya[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int j = 0; j < NROW; ++j) {
+            for (int j = 0; j < NR; ++j) {
                 if (!ron[j]) continue;
                 const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
                 const double rx = rho - rl[j] - rnu[j];
@@ -798,11 +803,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 break;
             }
             // -- barrier weights, augmented stage Hessians ---------------------------------------
-            double il[NROW], inu[NROW], wv[NROW], ilb[NBOX], wb[NBOX];
+            double il[NR], inu[NR], wv[NR], ilb[NBOX], wb[NBOX];
             {
                 double Qp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) {
+                for (int j = 0; j < NR; ++j) {
                     il[j] = frcp(rl[j]);
                     inu[j] = frcp(rnu[j]);
                     wv[j] = ron[j] ? frcp(fma(rs[j], il[j], rxi[j] * inu[j])) : 0.0;   // 1/d
@@ -832,9 +837,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             riccati_factor(S, N, dt, gl);
             PROF(5)
             // -- predictor, corrector (and, if needed, centred) solves ---------------------------------
-            double p4v[NROW], p5v[NROW], pbv[NBOX];
+            double p4v[NR], p5v[NR], pbv[NBOX];
 #pragma unroll
-            for (int j = 0; j < NROW; ++j) { p4v[j] = 0.0; p5v[j] = 0.0; }
+            for (int j = 0; j < NR; ++j) { p4v[j] = 0.0; p5v[j] = 0.0; }
 #pragma unroll
             for (int j = 0; j < NBOX; ++j) pbv[j] = 0.0;
             double sig = 0.0;
@@ -845,11 +850,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 const double smu = (pass >= 1) ? sig * mu : 0.0;
                 const double cw = (pass == 1) ? 1.0 : 0.0;     // weight of the second-order term
                 // reduced right-hand side per row, scaled by 1/d: wr = rh / d  (newton() of the oracle)
-                double wr[NROW], wrb[NBOX];
+                double wr[NR], wrb[NBOX];
                 {
                     double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
+                    for (int j = 0; j < NR; ++j) {
                         const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
                         const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
                         const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
@@ -883,10 +888,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
                 for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
                 const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
-                double dsv[NROW], dlv[NROW], dxv[NROW], dnv[NROW], dsb[NBOX], dlb[NBOX];
+                double dsv[NR], dlv[NR], dxv[NR], dnv[NR], dsb[NBOX], dlb[NBOX];
                 double amax = 1.0;
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) {
+                for (int j = 0; j < NR; ++j) {
                     const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
                     const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
                     const double rx = rho - rl[j] - rnu[j];
@@ -920,7 +925,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 const double a_try = (pass == 0) ? amax : fmin(1.0, TAU * amax);
                 double ca = 0.0;
 #pragma unroll
-                for (int j = 0; j < NROW; ++j)
+                for (int j = 0; j < NR; ++j)
                     if (ron[j])
                         ca += fma(a_try, dsv[j], rs[j]) * fma(a_try, dlv[j], rl[j]) +
                               fma(a_try, dxv[j], rxi[j]) * fma(a_try, dnv[j], rnu[j]);
@@ -933,7 +938,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double r = ca / comp;
                     sig = r * r * r;
 #pragma unroll
-                    for (int j = 0; j < NROW; ++j) { p4v[j] = dsv[j] * dlv[j]; p5v[j] = dxv[j] * dnv[j]; }
+                    for (int j = 0; j < NR; ++j) { p4v[j] = dsv[j] * dlv[j]; p5v[j] = dxv[j] * dnv[j]; }
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) pbv[j] = dsb[j] * dlb[j];
                     continue;
@@ -942,7 +947,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 const double alpha = a_try;
                 stall = (mu < 1e-6 && ca > 0.9 * comp) ? stall + 1 : 0;
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) {
+                for (int j = 0; j < NR; ++j) {
                     rs[j] = fma(alpha, dsv[j], rs[j]);
                     rl[j] = fma(alpha, dlv[j], rl[j]);
                     rxi[j] = fma(alpha, dxv[j], rxi[j]);
@@ -976,7 +981,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         } else if (st_here == MPC_OK) {
             double inf = 0.0;
 #pragma unroll
-            for (int j = 0; j < NROW; ++j)
+            for (int j = 0; j < NR; ++j)
                 if (ron[j] && rxi[j] > 1e-6 * (1.0 + fabs(bk[j]))) inf = 1.0;
             if (Q.max(inf) > 0.0) st_here = MPC_INFEASIBLE;
         }
@@ -986,9 +991,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         PROF(8)
         if (Pr.polish && bad == 0.0) {
             // class per row: 0 inactive, 1 active (equality), 2 violated (multiplier fixed at rho)
-            int cls[NROW], clb[NBOX];
+            int cls[NR], clb[NBOX];
 #pragma unroll
-            for (int j = 0; j < NROW; ++j) cls[j] = !ron[j] ? 0 : (rxi[j] > rnu[j] ? 2 : (rl[j] > rs[j] ? 1 : 0));
+            for (int j = 0; j < NR; ++j) cls[j] = !ron[j] ? 0 : (rxi[j] > rnu[j] ? 2 : (rl[j] > rs[j] ? 1 : 0));
 #pragma unroll
             for (int j = 0; j < NBOX; ++j) clb[j] = (live && lb[j] > sb[j]) ? 1 : 0;
             // the interior-point iterate (du, x4) is the start of every round and the fallback
@@ -996,15 +1001,15 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             bool accepted = false;
             double nviol_acc = 0.0;
             for (int round = 0; round < POLISH_ROUNDS; ++round) {
-                double tl[NROW], tlb[NBOX];
+                double tl[NR], tlb[NBOX];
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) tl[j] = rl[j];
+                for (int j = 0; j < NR; ++j) tl[j] = rl[j];
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j) tlb[j] = lb[j];
                 if (live) {
                     double Qp[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                    for (int j = 0; j < NROW; ++j) {
+                    for (int j = 0; j < NR; ++j) {
                         const double w = cls[j] == 1 ? 1.0 / POLISH_DELTA : 0.0;
 #pragma unroll
                         for (int a = 0; a < 4; ++a)
@@ -1028,15 +1033,15 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll 1
                 for (int r = 0; r < POLISH_REFINE; ++r) {
                     // exact KKT residual of the equality QP -> LQR right-hand side
-                    double r2[NROW], r2b[NBOX];
+                    double r2[NR], r2b[NBOX];
 #pragma unroll
-                    for (int j = 0; j < NROW; ++j) r2[j] = (cls[j] == 1) ? bk[j] - dot4(cf[j], xp) : 0.0;
+                    for (int j = 0; j < NR; ++j) r2[j] = (cls[j] == 1) ? bk[j] - dot4(cf[j], xp) : 0.0;
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) r2b[j] = (clb[j] == 1) ? bb[j] - bsign(j) * (j < 2 ? pu0 : pu1) : 0.0;
                     if (live) {
                         double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
-                        for (int j = 0; j < NROW; ++j) {
+                        for (int j = 0; j < NR; ++j) {
                             const double wgt = (cls[j] == 2) ? rho : (cls[j] == 1 ? tl[j] + r2[j] * (1.0 / POLISH_DELTA) : 0.0);
 #pragma unroll
                             for (int a = 0; a < 4; ++a)
@@ -1066,7 +1071,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
                         for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
 #pragma unroll
-                        for (int j = 0; j < NROW; ++j)
+                        for (int j = 0; j < NR; ++j)
                             if (cls[j] == 1) tl[j] += (r2[j] - dot4(cf[j], dx4)) * (1.0 / POLISH_DELTA);
                         const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
 #pragma unroll
@@ -1082,17 +1087,17 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 // acceptance: KKT consistency; otherwise flip every offending row and retry
                 double lmax = 1.0;
 #pragma unroll
-                for (int j = 0; j < NROW; ++j)
+                for (int j = 0; j < NR; ++j)
                     if (cls[j] == 1) lmax = fmax(lmax, fabs(tl[j]));
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j)
                     if (clb[j] == 1) lmax = fmax(lmax, fabs(tlb[j]));
                 lmax = Q.max(lmax);
                 double worst = 0.0, nviol = 0.0, finite = 1.0;
-                bool flip[NROW], flipb[NBOX];
+                bool flip[NR], flipb[NBOX];
                 if (live && (!(pu0 == pu0) || !(pu1 == pu1))) finite = 0.0;
 #pragma unroll
-                for (int j = 0; j < NROW; ++j) {
+                for (int j = 0; j < NR; ++j) {
                     flip[j] = false;
                     if (!ron[j]) continue;
                     const double bsc = 1.0 + fabs(bk[j]);
@@ -1133,7 +1138,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     break;
                 }
 #pragma unroll
-                for (int j = 0; j < NROW; ++j)
+                for (int j = 0; j < NR; ++j)
                     if (flip[j]) cls[j] = (cls[j] == 1) ? (tl[j] > rho ? 2 : 0) : 1;
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j)
@@ -1406,15 +1411,15 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
     const int G = WAVE / GL;
     const size_t lds_wave = lds * G;
     const dim3 grid((B + G - 1) / G);
-    if (GL == 16)
-        hipLaunchKernelGGL(mpc_solve_kernel<16>, grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, ubar,
-                           u0, U, Xpred, status, iters);
-    else if (GL == 32)
-        hipLaunchKernelGGL(mpc_solve_kernel<32>, grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, ubar,
-                           u0, U, Xpred, status, iters);
-    else
-        hipLaunchKernelGGL(mpc_solve_kernel<64>, grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, ubar,
-                           u0, U, Xpred, status, iters);
+    // obstacle rows exist only when obstacles are passed
+#define MPC_LAUNCH(GLV, OBSV)                                                                               \
+    hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV>), grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, \
+                       ubar, u0, U, Xpred, status, iters)
+    const bool with_obs = obs != nullptr && kp.max_obs > 0;
+    if (GL == 16) { if (with_obs) MPC_LAUNCH(16, true); else MPC_LAUNCH(16, false); }
+    else if (GL == 32) { if (with_obs) MPC_LAUNCH(32, true); else MPC_LAUNCH(32, false); }
+    else { if (with_obs) MPC_LAUNCH(64, true); else MPC_LAUNCH(64, false); }
+#undef MPC_LAUNCH
     HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
     return MPC_SUCCESS;
 }
