@@ -60,9 +60,11 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     dev = torch.device("cuda", local)
 
+    import shard
     cfg = W.CONFIGS[args.config]
     B = args.batch or cfg["B"] // max(1, cfg["gpus"])
-    wb = W.make_batch(args.config, B=B, offset=rank * B)
+    lo, hi = shard.shard_range(world * B, world, rank)      # weak scaling: B egos per GPU
+    wb = W.make_batch(args.config, B=hi - lo, offset=lo)
     N, mo = wb["N"], wb["max_obs"]
     X, U = W.loader(wb["traj"]).X_ref, W.loader(wb["traj"]).U_ref
     slv = mpcqp.Solver(X, U, mpcqp.default_params(N=N, max_obs=mo), device=local)
@@ -108,9 +110,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    iters = it.cpu().numpy()
-    status = st.cpu().numpy()
-    kmean = float(iters.mean())
+    # the one collective: gather of per-rank solver telemetry (after the timed region)
+    tel = shard.reduce_telemetry(shard.gather_telemetry(shard.telemetry(st.cpu().numpy(), it.cpu().numpy()),
+                                                        device=dev if world > 1 else None))
+    kmean = tel["mean_iters"]
     avg_launch_s = gpu_s / args.steps
     flops = algorithmic_flops(N, kmean) * B
     nbytes = algorithmic_bytes(N, mo) * B
@@ -140,8 +143,7 @@ def main():
             "config": {"workload": f"{args.config}: trajectory{wb['traj']}.json, N={N}, batch={B} egos per GPU, "
                                    f"max_obs={mo}, seed {cfg['seed']} (SURVEY 8d)", "global_batch": world * B,
                        "horizon": N, "parallelism": f"dp{world} (ego shards)"},
-            "solver": {"mean_iters": kmean, "max_iters": int(iters.max()),
-                       "status_counts": {mpcqp.STATUS_NAMES[k]: int((status == k).sum()) for k in range(4)}},
+            "solver": tel,
             "roofline": {"bound": "mfma", "achieved": flops / avg_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / avg_launch_s / 1e12 / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
