@@ -40,12 +40,14 @@ def make_batch(name, B=None, seed=None, offset=0):
     B = cfg["B"] if B is None else int(B)
     seed = cfg["seed"] if seed is None else seed
     ld = loader(cfg["traj"])
-    rng = np.random.default_rng(seed)
+    # one PCG64 stream per field (SeedSequence children), so that the egos [offset, offset+B) of a
+    # shard are exactly that slice of the single-process batch
+    rs = [np.random.default_rng(c) for c in np.random.SeedSequence(seed).spawn(8)]
     tot = offset + B
-    s0 = rng.uniform(0.0, 0.8 * ld.s_max, tot)
-    nd = rng.normal(0, 0.05, tot)
-    no = rng.normal(0, 0.01, tot)
-    nv = rng.normal(0, 0.5, tot)
+    s0 = rs[0].uniform(0.0, 0.8 * ld.s_max, tot)
+    nd = rs[1].normal(0, 0.05, tot)
+    no = rs[2].normal(0, 0.01, tot)
+    nv = rs[3].normal(0, 0.5, tot)
     x0 = np.empty((B, 5))
     for b in range(B):
         i = offset + b
@@ -56,8 +58,8 @@ def make_batch(name, B=None, seed=None, offset=0):
     max_obs = 0
     if kind in _FSM:
         max_obs = 2
-        pc = rng.uniform(size=tot)
-        pd = rng.uniform(8.0, 70.0, tot)
+        pc = rs[4].uniform(size=tot)
+        pd = rs[5].uniform(8.0, 70.0, tot)
         obs = np.zeros((B, 2, 2))
         n_obs = np.zeros(B, np.int32)
         f = _FSM[kind]
@@ -73,8 +75,8 @@ def make_batch(name, B=None, seed=None, offset=0):
             n_obs[b] = n
     elif kind == "const8":
         max_obs = 8
-        u = rng.uniform(0, 10, (tot, 8))
-        v = rng.uniform(2, 10, (tot, 8))
+        u = rs[6].uniform(0, 10, (tot, 8))
+        v = rs[7].uniform(2, 10, (tot, 8))
         obs = np.zeros((B, 8, 2))
         for b in range(B):
             i = offset + b
