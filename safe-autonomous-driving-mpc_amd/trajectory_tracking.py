@@ -25,8 +25,8 @@ from sanity_checks import trajectory_tracking_check
 # TrajectoryTracker attribute -> mpc_params field
 _PARAM_ATTRS = ("dt", "N", "vehicle_radius", "w_d", "w_o", "w_v", "w_u1", "w_u2", "obstacle_safety_distance",
                 "max_time_2_obs", "wheelbase", "lane_width", "safe_lane_margin")
-_SOLVER_ATTRS = ("linearization", "sqp_iters", "max_iter", "tol", "tol_mu", "elastic_rho", "brake_distance",
-                 "brake_accel")
+_SOLVER_ATTRS = ("linearization", "sqp_iters", "max_iter", "polish", "tol", "tol_mu", "elastic_rho",
+                 "brake_distance", "brake_accel")
 
 
 class TrajectoryTracker:
@@ -55,8 +55,9 @@ class TrajectoryTracker:
         self.linearization = 1
         self.sqp_iters = 1
         self.max_iter = 80
+        self.polish = 1
         self.tol = 1e-9
-        self.tol_mu = 1e-12
+        self.tol_mu = 1e-10
         self.elastic_rho = 1e5
         self.brake_distance = 40.0
         self.brake_accel = -2.0

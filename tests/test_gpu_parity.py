@@ -2,8 +2,10 @@
 and the CPU oracle.  Tolerances:
   lookups, warm start, nominal rollout / predict: bit-exact (FP64 integer-free arithmetic
       identical to numpy; the kernel is compiled with -ffp-contract=off);
-  QP(ubar) solution U*: <= 1e-7 abs vs the KKT-certified golden (the BASELINE gate is 1e-5)
-      and <= 1e-7 vs the oracle's PDIP on seeded batches of every configuration.
+  QP(ubar) solution U*: <= 5e-8 abs vs the KKT-certified golden (the BASELINE gate is 1e-5)
+      and <= 1e-6 vs the oracle's PDIP on seeded batches of every configuration (measured
+      4.8e-13 on the full C2 batch); status flips only between infeasible/numerical on badly
+      infeasible elastic problems, checked by objective value (check_vs_oracle).
 """
 import json
 
@@ -16,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 TOL_U = 1e-6          # GPU vs oracle (same PDIP); tightened once the active-set polish lands
 TOL_GATE = 1e-5       # BASELINE.json parity gate vs the certified golden
+TOL_CERT = 5e-8       # what the solver actually reaches vs the certified golden (oracle: 9.8e-9)
 
 
 @pytest.fixture(scope="module")
@@ -102,6 +105,7 @@ def test_qp_solution_vs_certified_golden(lib, solvers):
         err = float(np.abs(r["U"][0].ravel() - c["U_elastic"]).max())
         worst = max(worst, err)
         assert err <= TOL_GATE, (err, int(r["status"][0]), int(r["iters"][0]), json.loads(str(c["fdcheck"])))
+        assert err <= TOL_CERT, err
         if bool(c["feasible"]):
             assert int(r["status"][0]) == 0
         else:

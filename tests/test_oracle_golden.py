@@ -81,6 +81,9 @@ def golden_violation(orc, p, c):
     return float(max(0.0, np.max(q["lo"] - ax), np.max(ax - q["hi"])))
 
 
+TOL_QP = 5e-8      # measured worst 9.8e-9 over the 114 cases
+
+
 def test_qp_solution_vs_certified_golden(oracles):
     """Oracle PDIP vs the KKT-certified solution of QP(ubar) (hard QP when feasible == elastic)."""
     cases, g = golden_cases("qp_golden")
@@ -95,12 +98,13 @@ def test_qp_solution_vs_certified_golden(oracles):
         r = orc.solve(p, c["x0"], c["obs"], ubar=c["ubar"])
         err = np.abs(r["U"] - c["U_elastic"]).max()
         worst = max(worst, err)
-        assert err <= 1e-5, (err, r["status"], r["iters"], json.loads(str(c["kkt_elastic"])))
+        # BASELINE gate is 1e-5; the oracle agrees with the certified optimum to ~1e-8
+        assert err <= TOL_QP, (err, r["status"], r["iters"], json.loads(str(c["kkt_elastic"])))
         viol = golden_violation(orc, p, c)
         if bool(c["feasible"]):
             nfeas += 1
             assert r["status"] == 0, r
-            assert np.abs(r["U"] - c["U_hard"]).max() <= 1e-5
+            assert np.abs(r["U"] - c["U_hard"]).max() <= TOL_QP
         elif viol > 1e-5:
             assert r["status"] == 2, (r, viol)
         else:
