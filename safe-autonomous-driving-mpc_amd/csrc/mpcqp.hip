@@ -205,6 +205,15 @@ __device__ __forceinline__ double bsign(int j) { return (j & 1) ? -1.0 : 1.0; } 
 __device__ __forceinline__ double dot4(const double c[4], const double x[4]) {
     return fma(c[0], x[0], fma(c[1], x[1], fma(c[2], x[2], c[3] * x[3])));
 }
+// 1/sqrt(x) to full double precision: v_rsq_f64 + two Newton steps (the Cholesky pivots only
+// enter as reciprocals; the IEEE sqrt sequence costs ~100 cycles of dependent latency on gfx950)
+__device__ __forceinline__ double frsqrt(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
 // 1/x to full double precision: v_rcp_f64 + two Newton steps (no IEEE division sequence)
 __device__ __forceinline__ double frcp(double x) {
     double r = __builtin_amdgcn_rcp(x);
@@ -333,10 +342,10 @@ __device__ void riccati_factor(const Lds& S, int N, double dt, int ln) {
         // S = Rt + dt^2 P[{3,4},{3,4}] and its Cholesky factor
         double s00 = fma(dt2, P[s5(3, 3)], r0), s01 = dt2 * P[s5(3, 4)], s11 = fma(dt2, P[s5(4, 4)], r1);
         if (!(s00 > 0.0)) s00 = 1e-300 + fabs(s00);
-        const double l00 = sqrt(s00), il00 = frcp(l00), l10 = s01 * il00;
+        const double il00 = frsqrt(s00), l10 = s01 * il00;
         double r11 = s11 - l10 * l10;
         if (!(r11 > 1e-14 * s11)) r11 = 1e-14 * fabs(s11) + 1e-300;
-        const double l11 = sqrt(r11), il11 = frcp(l11);
+        const double il11 = frsqrt(r11);
         // M = P A  (A = I + J', J' sparse: a12, a14, a20, a23, a24, dt)
         double M[5][5];
 #pragma unroll

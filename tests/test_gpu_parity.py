@@ -170,6 +170,23 @@ def test_vs_oracle_seeded(lib, solvers, cfg, B):
     assert np.array_equal(r["u0"], r["U"][:, 0, :])
 
 
+@pytest.mark.parametrize("cfg,B,nsqp", [("C2", 256, 3), ("C3", 256, 2)])
+def test_sqp_relinearisation_vs_oracle(lib, solvers, cfg, B, nsqp):
+    """SQP outer iterations on device: QP(U*) re-linearised about the previous
+    solution, `sqp_iters` times; same fixed-point path as the oracle's orc_solve loop."""
+    import oracle as O
+    import workloads as W
+    wb = W.make_batch(cfg, B=B, seed=99)
+    slv = solvers[wb["traj"]]
+    set_p(lib, slv, wb["N"], wb["max_obs"], sqp_iters=nsqp)
+    r = slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
+    orc = O.Oracle(*traj_arrays(wb["traj"]))
+    po = O.default_params(N=wb["N"], max_obs=wb["max_obs"], sqp_iters=nsqp)
+    ro = orc.solve_batch(po, wb["x0"], wb["obs"], wb["n_obs"])
+    check_vs_oracle(r, ro, min_agree=0.97)
+    assert (r["iters"] >= nsqp).all()
+
+
 def test_full_size_C2_properties(lib, solvers):
     """BASELINE metric config (traj1, N=20, B=4096): size-independent properties + oracle subset."""
     import oracle as O
