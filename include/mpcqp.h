@@ -106,6 +106,30 @@ int mpc_lookup(mpc_ctx* c, int n, const double* s, double* out_state, double* ou
 int mpc_set_params(mpc_ctx* c, const mpc_params* p);
 int mpc_get_params(const mpc_ctx* c, mpc_params* p);
 
+/* ObstaclesFSM (trajectory_tracking.py:266-374): one dynamic car and one traffic light per ego.
+ * mpc_default_fsm() fills the trajectory2.json preset (:292-308) with both scenarios off. */
+typedef struct mpc_fsm {
+    int dynamic_obstacle, traffic_light;                        /* :286-288                   */
+    double obs_trigger_s, obs_start_s, obs_v, obs_end_s;        /* dynamic obstacle, :293-297 */
+    double tl_pos, tl_trigger_s, tl_stop_duration;              /* traffic light, :302-304    */
+} mpc_fsm;
+
+void mpc_default_fsm(mpc_fsm* f);
+
+/* Batched closed loop: run_simulation (trajectory_tracking.py:377-443) for B independent egos on the
+ * device.  Per step: ObstaclesFSM.update(dt, s, v) per ego, one batched solve, the Euler plant step
+ * x <- x + dt*dynamics(x, u0, k_ref(s)) (:403-406).  An ego leaves the loop once s > s_stop (the
+ * reference runs while s <= s_max - 1, :395); the call returns when every ego has left or after
+ * max_steps.  fsm may be NULL (no obstacles).  Host buffers (any history may be NULL):
+ *   x_init [B][5]; hist_x [B][max_steps+1][5] (row 0 = x_init); hist_u [B][max_steps][2];
+ *   hist_obs_s [B][max_steps] (car position, NaN if none); hist_tl [B][max_steps] (0 RED, 1 GREEN);
+ *   hist_status [B][max_steps] (solver status); n_steps [B] (steps each ego ran; required);
+ *   step_ms [max_steps] (wall time of each batched step on the device, NaN for steps not run).
+ * Entries past an ego's n_steps are NaN (doubles) / -1 (ints). */
+int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mpc_fsm* fsm, int max_steps, double s_stop,
+                    double* hist_x, double* hist_u, double* hist_obs_s, int* hist_tl, int* hist_status,
+                    int* n_steps, double* step_ms);
+
 /* Thread-local description of the last API error on this thread. */
 const char* mpc_last_error(void);
 int mpc_version(void);

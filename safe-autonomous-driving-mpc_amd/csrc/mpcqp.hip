@@ -1202,6 +1202,113 @@ __global__ void mpc_lookup_kernel(DevTable tab, int n, const double* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
+// batched closed loop: run_simulation, trajectory_tracking.py:377-443, per ego,
+// with the ObstaclesFSM of :266-374.  One thread per ego for the FSM and the plant; the solve in
+// between is the batched solver kernel.  Same arithmetic order as the reference (numpy), so a
+// closed loop on the device reproduces the host loop bit for bit.
+// ------------------------------------------------------------------------------------------
+struct ClState {
+    double* x;          // [B][5]    current state
+    double* obs;        // [B][2][2] obstacle slab of this step (car first, then the light: :341-358)
+    int* nobs;          // [B]
+    double* u0;         // [B][2]
+    int* status;        // [B]
+    int* active;        // [B]       still inside the loop condition s <= s_stop (:395)
+    double* obs_s;      // [B]       dynamic obstacle position
+    double* tl_timer;   // [B]
+    int* fsm_flags;     // [B][4]    obs_active, obs_has_triggered, tl_green, tl_waiting
+    int* n_active;      // [1]
+};
+
+// ObstaclesFSM.update(dt, s, v) (trajectory_tracking.py:330-374) for every active ego
+__global__ void cl_fsm_kernel(int B, mpc_fsm F, double dt, ClState C, double* hist_obs_s, int* hist_tl, int step,
+                              int max_steps) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    if (!C.active[b]) { C.nobs[b] = 0; return; }
+    const double s = C.x[5 * (size_t)b], v = C.x[5 * (size_t)b + 4];
+    int* fl = C.fsm_flags + 4 * (size_t)b;
+    double* o = C.obs + 4 * (size_t)b;
+    int n = 0;
+    double car_s = NAN;
+    if (F.dynamic_obstacle) {
+        if (!fl[1] && s >= F.obs_trigger_s) { fl[1] = 1; fl[0] = 1; }
+        if (fl[0]) {
+            const double os = C.obs_s[b] + F.obs_v * dt;
+            C.obs_s[b] = os;
+            if (os > F.obs_end_s) {
+                fl[0] = 0;
+            } else {
+                o[0] = os;
+                o[1] = F.obs_v;
+                n = 1;
+                car_s = os;
+            }
+        }
+    }
+    if (F.traffic_light && !fl[2]) {
+        const double dist = F.tl_pos - s;
+        if (0.0 < dist && dist < F.tl_trigger_s) {
+            o[2 * n] = F.tl_pos;
+            o[2 * n + 1] = 0.0;
+            ++n;
+            if (v < 0.1 && dist < 10.0) fl[3] = 1;
+        }
+        if (fl[3]) {
+            C.tl_timer[b] += dt;
+            if (C.tl_timer[b] >= F.tl_stop_duration) { fl[2] = 1; fl[3] = 0; }
+        }
+    }
+    C.nobs[b] = n;
+    if (hist_obs_s) hist_obs_s[(size_t)b * max_steps + step] = car_s;
+    if (hist_tl) hist_tl[(size_t)b * max_steps + step] = fl[2];
+}
+
+// plant step x <- x + dt * dynamics(x, u0, k_ref(x_s)) (:403-406) and the histories (:412-421)
+__global__ void cl_plant_kernel(DevTable tab, int B, double dt, ClState C, double s_stop, double* hist_x,
+                                double* hist_u, int* hist_status, int* n_steps, int step, int max_steps) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B || !C.active[b]) return;
+    double x[5], st[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) x[j] = C.x[5 * (size_t)b + j];
+    const double u1 = C.u0[2 * (size_t)b], u2 = C.u0[2 * (size_t)b + 1];
+    get_state(tab, x[0], st, nullptr);
+    const double xd[5] = {x[4], x[4] * x[2], x[4] * (x[3] - st[3]), u1, u2};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        x[j] = x[j] + dt * xd[j];
+        C.x[5 * (size_t)b + j] = x[j];
+        if (hist_x) hist_x[((size_t)b * (max_steps + 1) + step + 1) * 5 + j] = x[j];
+    }
+    if (hist_u) {
+        hist_u[((size_t)b * max_steps + step) * 2] = u1;
+        hist_u[((size_t)b * max_steps + step) * 2 + 1] = u2;
+    }
+    if (hist_status) hist_status[(size_t)b * max_steps + step] = C.status[b];
+    n_steps[b] = step + 1;
+    if (!(x[0] <= s_stop)) C.active[b] = 0;
+    else atomicAdd(C.n_active, 1);
+}
+
+__global__ void cl_init_kernel(int B, mpc_fsm F, ClState C, const double* x_init, double s_stop, double* hist_x,
+                               int* n_steps, int max_steps) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    for (int j = 0; j < 5; ++j) {
+        C.x[5 * (size_t)b + j] = x_init[5 * (size_t)b + j];
+        if (hist_x) hist_x[(size_t)b * (max_steps + 1) * 5 + j] = x_init[5 * (size_t)b + j];
+    }
+    C.active[b] = x_init[5 * (size_t)b] <= s_stop ? 1 : 0;
+    C.obs_s[b] = F.obs_start_s;
+    C.tl_timer[b] = 0.0;
+    for (int j = 0; j < 4; ++j) C.fsm_flags[4 * (size_t)b + j] = 0;
+    for (int j = 0; j < 4; ++j) C.obs[4 * (size_t)b + j] = 0.0;
+    C.nobs[b] = 0;
+    n_steps[b] = 0;
+}
+
+// ------------------------------------------------------------------------------------------
 // host side: C ABI
 // ------------------------------------------------------------------------------------------
 static thread_local std::string g_err = "";
@@ -1398,24 +1505,14 @@ extern "C" void mpc_destroy(mpc_ctx* c) {
     std::free(c);
 }
 
-extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const double* obs, const int* n_obs,
-                                      const double* ubar, double* u0, double* U, double* Xpred, int* status,
-                                      int* iters, void* stream) {
-    if (!c) return fail(MPC_E_ARG, "ctx is NULL");
-    if (B < 0) return fail(MPC_E_ARG, "B < 0");
-    if (B == 0) return MPC_SUCCESS;
-    if (!x0) return fail(MPC_E_ARG, "x0 is NULL");
-    if (c->p.max_obs > 0 && n_obs && !obs) return fail(MPC_E_ARG, "n_obs given but obs is NULL");
-    int rc = check_params(&c->p);
-    if (rc) return rc;
-    KParams kp = kparams(&c->p);
-    if (!obs) kp.max_obs = 0;
+// launch of the solver kernel for an already validated parameter set
+static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, const double* obs, const int* n_obs,
+                        const double* ubar, double* u0, double* U, double* Xpred, int* status, int* iters,
+                        hipStream_t st) {
     size_t lds = sizeof(double) * (size_t)lds_doubles(kp.N);
     if (lds > 160 * 1024) return fail(MPC_E_ARG, "horizon too long for LDS");
-    HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
     // G = 64 / GL instances per wavefront: the smallest lane group holding the N + 1 stages
     const int* nob = obs ? n_obs : nullptr;
-    hipStream_t st = (hipStream_t)stream;
     const int GL = kp.N + 1 <= 16 ? 16 : (kp.N + 1 <= 32 ? 32 : 64);
     const int G = WAVE / GL;
     const size_t lds_wave = lds * G;
@@ -1431,6 +1528,22 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
 #undef MPC_LAUNCH
     HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
     return MPC_SUCCESS;
+}
+
+extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const double* obs, const int* n_obs,
+                                      const double* ubar, double* u0, double* U, double* Xpred, int* status,
+                                      int* iters, void* stream) {
+    if (!c) return fail(MPC_E_ARG, "ctx is NULL");
+    if (B < 0) return fail(MPC_E_ARG, "B < 0");
+    if (B == 0) return MPC_SUCCESS;
+    if (!x0) return fail(MPC_E_ARG, "x0 is NULL");
+    if (c->p.max_obs > 0 && n_obs && !obs) return fail(MPC_E_ARG, "n_obs given but obs is NULL");
+    int rc = check_params(&c->p);
+    if (rc) return rc;
+    KParams kp = kparams(&c->p);
+    if (!obs) kp.max_obs = 0;
+    HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
+    return launch_solve(c, kp, B, x0, obs, n_obs, ubar, u0, U, Xpred, status, iters, (hipStream_t)stream);
 }
 
 template <typename T>
@@ -1489,6 +1602,132 @@ extern "C" int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double
     if (iters) HIPCHK(hipMemcpyAsync(iters, c->iters, sizeof(int) * B, hipMemcpyDeviceToHost, s), MPC_E_DEVICE);
     HIPCHK(hipStreamSynchronize(s), MPC_E_DEVICE);
     return MPC_SUCCESS;
+}
+
+extern "C" void mpc_default_fsm(mpc_fsm* f) {
+    std::memset(f, 0, sizeof(*f));
+    // the trajectory2.json preset, active in the reference (trajectory_tracking.py:292-308)
+    f->obs_trigger_s = 710.0;
+    f->obs_start_s = 780.0;
+    f->obs_v = 4.0;
+    f->obs_end_s = 1050.0;
+    f->tl_pos = 550.0;
+    f->tl_trigger_s = 100.0;
+    f->tl_stop_duration = 20.0;
+}
+
+extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mpc_fsm* fsm, int max_steps,
+                               double s_stop, double* hist_x, double* hist_u, double* hist_obs_s, int* hist_tl,
+                               int* hist_status, int* n_steps, double* step_ms) {
+    if (!c) return fail(MPC_E_ARG, "ctx is NULL");
+    if (B < 0 || max_steps < 1) return fail(MPC_E_ARG, "B < 0 or max_steps < 1");
+    if (B == 0) return MPC_SUCCESS;
+    if (!x_init || !n_steps) return fail(MPC_E_ARG, "x_init and n_steps are required");
+    int rc = check_params(&c->p);
+    if (rc) return rc;
+    mpc_fsm F;
+    if (fsm) F = *fsm; else mpc_default_fsm(&F);     // NULL: both scenarios off
+    const bool with_fsm = fsm && (F.dynamic_obstacle || F.traffic_light);
+    KParams kp = kparams(&c->p);
+    kp.max_obs = with_fsm ? 2 : 0;          // the FSM yields at most the car and the light
+    HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
+    const size_t nb = (size_t)B, ns = (size_t)max_steps;
+    std::vector<void*> bufs;
+    auto dalloc = [&](size_t bytes) -> void* {
+        void* ptr = nullptr;
+        if (hipMalloc(&ptr, bytes) != hipSuccess) return nullptr;
+        bufs.push_back(ptr);
+        return ptr;
+    };
+    auto release = [&]() { for (void* q : bufs) hipFree(q); };
+    ClState C;
+    C.x = (double*)dalloc(nb * 5 * 8);
+    C.obs = (double*)dalloc(nb * 4 * 8);
+    C.nobs = (int*)dalloc(nb * 4);
+    C.u0 = (double*)dalloc(nb * 2 * 8);
+    C.status = (int*)dalloc(nb * 4);
+    C.active = (int*)dalloc(nb * 4);
+    C.obs_s = (double*)dalloc(nb * 8);
+    C.tl_timer = (double*)dalloc(nb * 8);
+    C.fsm_flags = (int*)dalloc(nb * 4 * 4);
+    C.n_active = (int*)dalloc(4);
+    double* d_xinit = (double*)dalloc(nb * 5 * 8);
+    double* d_hx = hist_x ? (double*)dalloc(nb * (ns + 1) * 5 * 8) : nullptr;
+    double* d_hu = hist_u ? (double*)dalloc(nb * ns * 2 * 8) : nullptr;
+    double* d_ho = hist_obs_s ? (double*)dalloc(nb * ns * 8) : nullptr;
+    int* d_ht = hist_tl ? (int*)dalloc(nb * ns * 4) : nullptr;
+    int* d_hs = hist_status ? (int*)dalloc(nb * ns * 4) : nullptr;
+    int* d_ns = (int*)dalloc(nb * 4);
+    for (void* q : bufs)
+        if (!q) { release(); return fail(MPC_E_ALLOC, "hipMalloc closed-loop buffers"); }
+    if ((hist_x && !d_hx) || (hist_u && !d_hu) || (hist_obs_s && !d_ho) || (hist_tl && !d_ht) || (hist_status && !d_hs)) {
+        release();
+        return fail(MPC_E_ALLOC, "hipMalloc closed-loop histories");
+    }
+    hipStream_t st = c->stream;
+    // steps that never run stay NaN / -1 (all-ones bytes)
+    if (d_hx) hipMemsetAsync(d_hx, 0xff, nb * (ns + 1) * 5 * 8, st);
+    if (d_hu) hipMemsetAsync(d_hu, 0xff, nb * ns * 2 * 8, st);
+    if (d_ho) hipMemsetAsync(d_ho, 0xff, nb * ns * 8, st);
+    if (d_ht) hipMemsetAsync(d_ht, 0xff, nb * ns * 4, st);
+    if (d_hs) hipMemsetAsync(d_hs, 0xff, nb * ns * 4, st);
+    if (hipMemcpyAsync(d_xinit, x_init, nb * 5 * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
+        release();
+        return fail(MPC_E_DEVICE, "hipMemcpy x_init");
+    }
+    const dim3 tb(256), tg((B + 255) / 256);
+    hipLaunchKernelGGL(cl_init_kernel, tg, tb, 0, st, B, F, C, d_xinit, s_stop, d_hx, d_ns, max_steps);
+    std::vector<hipEvent_t> ev;
+    if (step_ms) {
+        ev.resize(ns + 1);
+        for (auto& e : ev) hipEventCreate(&e);
+        hipEventRecord(ev[0], st);
+    }
+    int steps_run = 0;
+    rc = MPC_SUCCESS;
+    for (int step = 0; step < max_steps; ++step) {
+        // runs without scenarios too: records the RED light / no-car histories like the reference
+        hipLaunchKernelGGL(cl_fsm_kernel, tg, tb, 0, st, B, F, kp.dt, C, d_ho, d_ht, step, max_steps);
+        rc = launch_solve(c, kp, B, C.x, with_fsm ? C.obs : nullptr, with_fsm ? C.nobs : nullptr, nullptr, C.u0,
+                          nullptr, nullptr, C.status, nullptr, st);
+        if (rc) break;
+        hipMemsetAsync(C.n_active, 0, 4, st);
+        hipLaunchKernelGGL(cl_plant_kernel, tg, tb, 0, st, c->tab, B, kp.dt, C, s_stop, d_hx, d_hu, d_hs, d_ns, step,
+                           max_steps);
+        if (step_ms) hipEventRecord(ev[step + 1], st);
+        steps_run = step + 1;
+        if ((step & 7) == 7 || step == max_steps - 1) {     // every 8 steps: has every ego left the loop?
+            int na = 0;
+            if (hipMemcpyAsync(&na, C.n_active, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                rc = fail(MPC_E_DEVICE, "closed-loop step sync");
+                break;
+            }
+            if (na == 0) break;
+        }
+    }
+    if (rc == MPC_SUCCESS && hipGetLastError() != hipSuccess) rc = fail(MPC_E_LAUNCH, "closed-loop kernel launch");
+    if (rc == MPC_SUCCESS) {
+        bool ok = hipMemcpyAsync(n_steps, d_ns, nb * 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+        if (hist_x) ok = ok && hipMemcpyAsync(hist_x, d_hx, nb * (ns + 1) * 5 * 8, hipMemcpyDeviceToHost, st) == hipSuccess;
+        if (hist_u) ok = ok && hipMemcpyAsync(hist_u, d_hu, nb * ns * 2 * 8, hipMemcpyDeviceToHost, st) == hipSuccess;
+        if (hist_obs_s) ok = ok && hipMemcpyAsync(hist_obs_s, d_ho, nb * ns * 8, hipMemcpyDeviceToHost, st) == hipSuccess;
+        if (hist_tl) ok = ok && hipMemcpyAsync(hist_tl, d_ht, nb * ns * 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+        if (hist_status) ok = ok && hipMemcpyAsync(hist_status, d_hs, nb * ns * 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+        ok = ok && hipStreamSynchronize(st) == hipSuccess;
+        if (!ok) rc = fail(MPC_E_DEVICE, "closed-loop copy-back");
+    }
+    if (step_ms) {
+        for (size_t i = 0; i < ns; ++i) {
+            float ms = NAN;
+            if ((int)i < steps_run) hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+            step_ms[i] = ms;
+        }
+        for (auto& e : ev) hipEventDestroy(e);
+    }
+    hipStreamSynchronize(st);
+    release();
+    return rc;
 }
 
 extern "C" int mpc_lookup(mpc_ctx* c, int n, const double* s, double* out_state, double* out_control) {

@@ -36,12 +36,21 @@ class MpcParams(C.Structure):
     ]
 
 
+class MpcFsm(C.Structure):
+    """`mpc_fsm` of include/mpcqp.h (ObstaclesFSM parameters, trajectory_tracking.py:286-304)."""
+    _fields_ = [("dynamic_obstacle", C.c_int), ("traffic_light", C.c_int),
+                ("obs_trigger_s", C.c_double), ("obs_start_s", C.c_double), ("obs_v", C.c_double),
+                ("obs_end_s", C.c_double), ("tl_pos", C.c_double), ("tl_trigger_s", C.c_double),
+                ("tl_stop_duration", C.c_double)]
+
+
 class MpcError(RuntimeError):
     pass
 
 
 EXPORTS = ["mpc_default_params", "mpc_create", "mpc_solve_batch", "mpc_solve_batch_device", "mpc_lookup",
-           "mpc_set_params", "mpc_get_params", "mpc_last_error", "mpc_version", "mpc_destroy"]
+           "mpc_set_params", "mpc_get_params", "mpc_last_error", "mpc_version", "mpc_destroy", "mpc_default_fsm",
+           "mpc_closed_loop"]
 
 _lib = None
 
@@ -71,6 +80,10 @@ def lib():
     L.mpc_last_error.restype = C.c_char_p
     L.mpc_version.restype = C.c_int
     L.mpc_destroy.argtypes = [C.c_void_p]
+    L.mpc_default_fsm.argtypes = [C.POINTER(MpcFsm)]
+    L.mpc_closed_loop.restype = C.c_int
+    L.mpc_closed_loop.argtypes = [C.c_void_p, C.c_int, _dp, C.POINTER(MpcFsm), C.c_int, C.c_double, _dp, _dp, _dp,
+                                  _ip, _ip, _ip, _dp]
     _lib = L
     return L
 
@@ -89,6 +102,14 @@ def default_params(**kw):
         else:
             setattr(p, k, v)
     return p
+
+
+def default_fsm(**kw):
+    f = MpcFsm()
+    lib().mpc_default_fsm(C.byref(f))
+    for k, v in kw.items():
+        setattr(f, k, v)
+    return f
 
 
 def _p(a):
@@ -158,6 +179,25 @@ class Solver:
         """Device-pointer variant (ints are raw device addresses, e.g. torch tensor.data_ptr())."""
         _check(lib().mpc_solve_batch_device(self.h, int(B), x0_ptr, obs_ptr, nobs_ptr, ubar_ptr, u0_ptr, U_ptr,
                                             X_ptr, st_ptr, it_ptr, C.c_void_p(stream)), "mpc_solve_batch_device")
+
+    def closed_loop(self, x_init, fsm=None, max_steps=1000, s_stop=None, s_max=None):
+        """Batched run_simulation (trajectory_tracking.py:377-443) on the device.
+        x_init [B,5]; fsm: MpcFsm or None; the loop runs while s <= s_stop (default s_max - 1, :395).
+        Returns dict(hist_x [B,max_steps+1,5], hist_u [B,max_steps,2], hist_obs_s [B,max_steps],
+        hist_tl [B,max_steps], hist_status [B,max_steps], n_steps [B], step_ms [max_steps])."""
+        x_init = np.ascontiguousarray(x_init, np.float64).reshape(-1, 5)
+        B = x_init.shape[0]
+        if s_stop is None:
+            if s_max is None:
+                raise ValueError("give s_stop or s_max")
+            s_stop = s_max - 1.0
+        hx = np.empty((B, max_steps + 1, 5)); hu = np.empty((B, max_steps, 2)); ho = np.empty((B, max_steps))
+        ht = np.empty((B, max_steps), np.int32); hs = np.empty((B, max_steps), np.int32)
+        ns = np.empty(B, np.int32); sm = np.empty(max_steps)
+        _check(lib().mpc_closed_loop(self.h, B, _p(x_init), None if fsm is None else C.byref(fsm), int(max_steps),
+                                     float(s_stop), _p(hx), _p(hu), _p(ho), _pi(ht), _pi(hs), _pi(ns), _p(sm)),
+               "mpc_closed_loop")
+        return dict(hist_x=hx, hist_u=hu, hist_obs_s=ho, hist_tl=ht, hist_status=hs, n_steps=ns, step_ms=sm)
 
     def lookup(self, s):
         s = np.ascontiguousarray(s, np.float64).ravel()

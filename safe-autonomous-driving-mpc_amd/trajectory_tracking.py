@@ -260,6 +260,47 @@ def run_simulation(mpc, fsm, trajectory, max_steps=None, verbose=True):
             trajectory)
 
 
+def fsm_params(fsm):
+    """mpc_fsm (include/mpcqp.h) of an ObstaclesFSM, or None when it has no scenario switched on."""
+    if fsm is None or not (fsm.dynamic_obstacle or fsm.traffic_light):
+        return None
+    return mpcqp.default_fsm(dynamic_obstacle=int(bool(fsm.dynamic_obstacle)), traffic_light=int(bool(fsm.traffic_light)),
+                             **{k: float(getattr(fsm, k)) for k in FSM_PRESETS["trajectory2"]})
+
+
+def run_simulation_batch(mpc, fsm, trajectory, x_init=None, B=1, max_steps=2000, checks=False, verbose=False):
+    """run_simulation (trajectory_tracking.py:377-443) for B independent egos, entirely on the device
+    (mpc_closed_loop): each ego owns a fresh copy of `fsm`'s scenario, the loop runs while
+    s <= s_max - 1.  x_init [B,5] defaults to the reference start [0,0,0,0,0.5] (:382).
+    Returns the device histories (see mpcqp.Solver.closed_loop); with checks=True also runs the
+    restated trajectory_tracking_check on every ego and adds 'checks_passed' [B]."""
+    if x_init is None:
+        x_init = np.tile(np.array([0.0, 0.0, 0.0, 0.0, 0.5]), (B, 1))
+    x_init = np.asarray(x_init, np.float64).reshape(-1, 5)
+    r = mpc.solver(max_obs=0).closed_loop(x_init, fsm_params(fsm), max_steps=max_steps, s_max=trajectory.s_max)
+    if checks:
+        import contextlib
+        import io
+        ok = np.zeros(x_init.shape[0], bool)
+        for b in range(x_init.shape[0]):
+            n = int(r["n_steps"][b])
+            step_s = np.full(n, np.nanmedian(r["step_ms"][:n]) / 1e3 / x_init.shape[0]) if n else np.zeros(0)
+            f = ObstaclesFSM(fsm.dynamic_obstacle, fsm.traffic_light) if fsm is not None else ObstaclesFSM()
+            if fsm is not None:
+                for k in FSM_PRESETS["trajectory2"]:
+                    setattr(f, k, getattr(fsm, k))
+            buf = io.StringIO()
+            tl = ["GREEN" if t == 1 else "RED" for t in r["hist_tl"][b, :n]]
+            with contextlib.redirect_stdout(buf):
+                ok[b] = bool(trajectory_tracking_check(mpc, list(r["hist_x"][b, :n + 1]), list(r["hist_u"][b, :n]),
+                                                       list(step_s), list(r["hist_obs_s"][b, :n]), tl, f,
+                                                       trajectory.s_max))
+            if verbose:
+                print(buf.getvalue())
+        r["checks_passed"] = ok
+    return r
+
+
 if __name__ == "__main__":
     from trajectory_loader import TrajectoryLoader, builtin_trajectory
     traj = TrajectoryLoader(builtin_trajectory(2))

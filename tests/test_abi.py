@@ -31,7 +31,8 @@ def built():
 def test_header_declares_the_boundary():
     names = declared_functions()
     for n in ("mpc_create", "mpc_solve_batch", "mpc_solve_batch_device", "mpc_last_error", "mpc_destroy",
-              "mpc_default_params", "mpc_lookup", "mpc_set_params", "mpc_get_params", "mpc_version"):
+              "mpc_default_params", "mpc_lookup", "mpc_set_params", "mpc_get_params", "mpc_version",
+              "mpc_default_fsm", "mpc_closed_loop"):
         assert n in names
 
 
@@ -106,3 +107,18 @@ def test_shim_surface_matches_reference():
     f = TT.ObstaclesFSM(dynamic_obstacle=True, traffic_light=True)
     obs, st = f.update(0.2, 0.0, 1.0)
     assert obs == [] and st == "RED"
+
+
+def test_fsm_struct_defaults(built):
+    """mpc_fsm mirrors ObstaclesFSM.__init__ (trajectory_tracking.py:286-304, trajectory2 preset)."""
+    import mpcqp
+    import trajectory_tracking as TT
+    f = mpcqp.default_fsm()
+    assert f.dynamic_obstacle == 0 and f.traffic_light == 0
+    for k, v in TT.FSM_PRESETS["trajectory2"].items():
+        assert getattr(f, k) == v, k
+    g = TT.fsm_params(TT.ObstaclesFSM(dynamic_obstacle=True, traffic_light=False, preset="trajectory3"))
+    assert g.dynamic_obstacle == 1 and g.traffic_light == 0 and g.obs_trigger_s == 5.0 and g.tl_pos == 2000.0
+    assert TT.fsm_params(TT.ObstaclesFSM()) is None
+    rc = mpcqp.lib().mpc_closed_loop(None, 1, None, None, 10, 0.0, None, None, None, None, None, None, None)
+    assert rc == -1 and "ctx" in mpcqp.last_error()
