@@ -753,6 +753,12 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         PROF(0)
         for (int iter = 0; iter < Pr.max_iter; ++iter) {
             PROF(1)
+            // the row bounds are loop-invariant; keeping them opaque stops the compiler from hoisting
+            // everything derived from them out of this loop (it would stay live in registers and spill)
+#pragma unroll
+            for (int j = 0; j < NR; ++j) asm volatile("" : "+v"(bk[j]));
+#pragma unroll
+            for (int j = 0; j < NBOX; ++j) asm volatile("" : "+v"(bb[j]));
             // -- stage-parallel residuals ------------------------------------------------------
             double rpmax = 0.0, rxmax = 0.0, comp = 0.0;
             double ya[4] = {0, 0, 0, 0};
@@ -999,6 +1005,13 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         // ---- active-set polish (oracle polish()) --------------------------
         PROF(8)
         if (Pr.polish && bad == 0.0) {
+            // opaque copies of the row bounds (see the interior-point loop): nothing the polish derives
+            // from them is hoisted into long-lived registers
+            double bkp[NR], bbp[NBOX];
+#pragma unroll
+            for (int j = 0; j < NR; ++j) { bkp[j] = bk[j]; asm volatile("" : "+v"(bkp[j])); }
+#pragma unroll
+            for (int j = 0; j < NBOX; ++j) { bbp[j] = bb[j]; asm volatile("" : "+v"(bbp[j])); }
             // class per row: 0 inactive, 1 active (equality), 2 violated (multiplier fixed at rho)
             int cls[NR], clb[NBOX];
 #pragma unroll
@@ -1044,9 +1057,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     // exact KKT residual of the equality QP -> LQR right-hand side
                     double r2[NR], r2b[NBOX];
 #pragma unroll
-                    for (int j = 0; j < NR; ++j) r2[j] = (cls[j] == 1) ? bk[j] - dot4(cf[j], xp) : 0.0;
+                    for (int j = 0; j < NR; ++j) r2[j] = (cls[j] == 1) ? bkp[j] - dot4(cf[j], xp) : 0.0;
 #pragma unroll
-                    for (int j = 0; j < NBOX; ++j) r2b[j] = (clb[j] == 1) ? bb[j] - bsign(j) * (j < 2 ? pu0 : pu1) : 0.0;
+                    for (int j = 0; j < NBOX; ++j) r2b[j] = (clb[j] == 1) ? bbp[j] - bsign(j) * (j < 2 ? pu0 : pu1) : 0.0;
                     if (live) {
                         double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
@@ -1109,8 +1122,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 for (int j = 0; j < NR; ++j) {
                     flip[j] = false;
                     if (!ron[j]) continue;
-                    const double bsc = 1.0 + fabs(bk[j]);
-                    const double r = dot4(cf[j], xp) - bk[j];
+                    const double bsc = 1.0 + fabs(bkp[j]);
+                    const double r = dot4(cf[j], xp) - bkp[j];
                     double badv = 0.0;
                     if (cls[j] == 1) {
                         if (tl[j] < -1e-9 * lmax) badv = -tl[j] / lmax;
@@ -1127,8 +1140,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 for (int j = 0; j < NBOX; ++j) {
                     flipb[j] = false;
                     if (!live) continue;
-                    const double bsc = 1.0 + fabs(bb[j]);
-                    const double r = bsign(j) * (j < 2 ? pu0 : pu1) - bb[j];
+                    const double bsc = 1.0 + fabs(bbp[j]);
+                    const double r = bsign(j) * (j < 2 ? pu0 : pu1) - bbp[j];
                     double badv = 0.0;
                     if (clb[j] == 1) {
                         if (tlb[j] < -1e-9 * lmax) badv = -tlb[j] / lmax;
