@@ -102,6 +102,20 @@ int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const double* ob
  * (trajectory_loader.py:86-102), batched. Host buffers, synchronous.  out_state [n][5], out_control [n][2]. */
 int mpc_lookup(mpc_ctx* c, int n, const double* s, double* out_state, double* out_control);
 
+/* TrajectoryLoader.get_global_pose(s, d) (trajectory_loader.py:104-116), batched: Frenet (s, d) ->
+ * global (x, y, psi) of the reference line built at mpc_create (trajectory_loader.py:32-62).
+ * Host buffers, synchronous.  out [n][3]. */
+int mpc_global_pose(mpc_ctx* c, int n, const double* s, const double* d, double* out);
+
+/* Read a trajectory JSON in the reference's format ({"X": [[s,d,o,k,v],...], "U": [[u1,u2],...]},
+ * trajectory_loader.py:13-24; other keys ignored).  Two-call pattern: with X == U == NULL only the
+ * sizes T, Tu are returned; then X [T][5] and U [Tu][2] (capacities maxT, maxTu rows) are filled.
+ * Host only, no device needed.  A missing file is MPC_E_ARG ("File not found : <path>."). */
+int mpc_read_trajectory_json(const char* path, double* X, int maxT, double* U, int maxTu, int* T, int* Tu);
+
+/* mpc_read_trajectory_json + mpc_create: replaces TrajectoryLoader(json_file) + TrajectoryTracker(X_ref). */
+int mpc_create_from_json(const char* path, const mpc_params* p, int device, mpc_ctx** out);
+
 /* Change parameters of an existing context (e.g. TrajectoryTracker.N = 20 after construction). */
 int mpc_set_params(mpc_ctx* c, const mpc_params* p);
 int mpc_get_params(const mpc_ctx* c, mpc_params* p);

@@ -37,6 +37,7 @@
 struct orc_table {
     int T, Tu;
     double *s, *d, *o, *k, *v, *u1, *u2;
+    double *gx, *gy, *gpsi;             /* global geometry, trajectory_loader.py:32-62 */
     double smax;
     double last[5];
 };
@@ -66,14 +67,18 @@ void orc_default_params(mpc_params* p) {
     p->polish = 1;
 }
 
+static int seg(const double* x, int n, double v);
+static double lin(const double* x, const double* y, int i, double v);
+
 orc_table* orc_table_create(const double* X, int T, const double* U, int Tu) {
     if (T < 2 || Tu < 1) return NULL;
     orc_table* t = (orc_table*)calloc(1, sizeof(orc_table));
     t->T = T;
     t->Tu = Tu < T ? Tu : T;            /* limit = min(len(s), len(U))  trajectory_loader.py:73-75 */
-    double* buf = (double*)malloc(sizeof(double) * (5 * T + 2 * t->Tu));
+    double* buf = (double*)malloc(sizeof(double) * (8 * T + 2 * t->Tu));
     t->s = buf; t->d = buf + T; t->o = buf + 2 * T; t->k = buf + 3 * T; t->v = buf + 4 * T;
     t->u1 = buf + 5 * T; t->u2 = buf + 5 * T + t->Tu;
+    t->gx = buf + 5 * T + 2 * t->Tu; t->gy = t->gx + T; t->gpsi = t->gy + T;
     for (int i = 0; i < T; ++i) {
         double si = X[5 * i];
         if (i > 0 && si <= t->s[i - 1]) si = t->s[i - 1] + 1e-5;   /* trajectory_loader.py:28-30 */
@@ -83,7 +88,31 @@ orc_table* orc_table_create(const double* X, int T, const double* U, int Tu) {
     for (int i = 0; i < t->Tu; ++i) { t->u1[i] = U[2 * i]; t->u2[i] = U[2 * i + 1]; }
     t->smax = t->s[T - 1];
     for (int j = 0; j < 5; ++j) t->last[j] = X[5 * (T - 1) + j];
+    /* global pose of the reference line: heading integrates the planned curvature X[i-1,3] over ds,
+     * position integrates the mean heading of each step (trajectory_loader.py:38-58) */
+    t->gx[0] = t->gy[0] = t->gpsi[0] = 0.0;
+    for (int i = 1; i < T; ++i) {
+        double ds = t->s[i] - t->s[i - 1];
+        double kk = X[5 * (i - 1) + 3];
+        double psi_old = t->gpsi[i - 1];
+        double psi_new = psi_old + kk * ds;
+        double psi_avg = (psi_old + psi_new) / 2.0;
+        t->gpsi[i] = psi_new;
+        t->gx[i] = t->gx[i - 1] + cos(psi_avg) * ds;
+        t->gy[i] = t->gy[i - 1] + sin(psi_avg) * ds;
+    }
     return t;
+}
+
+/* TrajectoryLoader.get_global_pose(s, d) (trajectory_loader.py:104-116): clamp s to s_max, interpolate
+ * the global line (linear, extrapolating below 0), offset laterally by d. */
+void orc_global_pose(const orc_table* t, double s, double d, double out[3]) {
+    if (s > t->smax) s = t->smax;
+    int i = seg(t->s, t->T, s);
+    double xr = lin(t->s, t->gx, i, s), yr = lin(t->s, t->gy, i, s), psi = lin(t->s, t->gpsi, i, s);
+    out[0] = xr - d * sin(psi);
+    out[1] = yr + d * cos(psi);
+    out[2] = psi;
 }
 
 void orc_table_destroy(orc_table* t) {

@@ -31,6 +31,8 @@ double orc_s_max(const orc_table* t);
 /* trajectory_loader.py:86-102 */
 void orc_get_state(const orc_table* t, double s, double out[5]);
 void orc_get_control(const orc_table* t, double s, double out[2]);
+/* TrajectoryLoader.get_global_pose (trajectory_loader.py:32-62,104-116) -> (x, y, psi) */
+void orc_global_pose(const orc_table* t, double s, double d, double out[3]);
 /* the interp1d segment slopes of (d,o,k,v) at s (0 for s >= s_max): Gauss-Newton data */
 void orc_state_slopes(const orc_table* t, double s, double out[4]);
 

@@ -54,6 +54,7 @@ def lib():
         L.orc_get_state.argtypes = [C.c_void_p, C.c_double, _dp]
         L.orc_get_control.argtypes = [C.c_void_p, C.c_double, _dp]
         L.orc_state_slopes.argtypes = [C.c_void_p, C.c_double, _dp]
+        L.orc_global_pose.argtypes = [C.c_void_p, C.c_double, C.c_double, _dp]
         L.orc_warm_start.argtypes = [C.c_void_p, C.POINTER(MpcParams), _dp, _dp, C.c_int, _dp]
         L.orc_predict.argtypes = [C.c_void_p, C.POINTER(MpcParams), _dp, _dp, _dp]
         L.orc_cost.restype = C.c_double
@@ -122,6 +123,11 @@ class Oracle:
     def get_control(self, s):
         out = np.zeros(2)
         lib().orc_get_control(self.h, float(s), _p(out))
+        return out
+
+    def global_pose(self, s, d):
+        out = np.zeros(3)
+        lib().orc_global_pose(self.h, float(s), float(d), _p(out))
         return out
 
     def state_slopes(self, s):

@@ -43,6 +43,9 @@ struct DevTable {
     const double* v;
     const double* u1;  // [Tu]
     const double* u2;
+    const double* gx;  // [T]  global pose of the reference line (trajectory_loader.py:32-62)
+    const double* gy;
+    const double* gpsi;
     int T, Tu;
     double smax;
     double last[5];    // X_ref[-1] verbatim (trajectory_loader.py:90-91)
@@ -1321,6 +1324,20 @@ __global__ void cl_init_kernel(int B, mpc_fsm F, ClState C, const double* x_init
     n_steps[b] = 0;
 }
 
+// TrajectoryLoader.get_global_pose(s, d) (trajectory_loader.py:104-116), batched
+__global__ void mpc_pose_kernel(DevTable tab, int n, const double* __restrict__ s, const double* __restrict__ d,
+                                double* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double si = s[i];
+    if (si > tab.smax) si = tab.smax;
+    const int j = seg(tab.s, tab.T, si);
+    const double xr = lin(tab.s, tab.gx, j, si), yr = lin(tab.s, tab.gy, j, si), psi = lin(tab.s, tab.gpsi, j, si);
+    out[3 * (size_t)i] = xr - d[i] * sin(psi);
+    out[3 * (size_t)i + 1] = yr + d[i] * cos(psi);
+    out[3 * (size_t)i + 2] = psi;
+}
+
 // ------------------------------------------------------------------------------------------
 // host side: C ABI
 // ------------------------------------------------------------------------------------------
@@ -1440,7 +1457,7 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     if (device < 0 || device >= ndev) return fail(MPC_E_DEVICE, "device index out of range");
     HIPCHK(hipSetDevice(device), MPC_E_DEVICE);
     int tu = Tu < T ? Tu : T;   // limit = min(len(s), len(U))   trajectory_loader.py:73-75
-    std::vector<double> h((size_t)5 * T + 2 * tu);
+    std::vector<double> h((size_t)8 * T + 2 * tu);
     double* s = h.data();
     for (int i = 0; i < T; ++i) {
         double si = X[5 * i];
@@ -1452,6 +1469,21 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         h[4 * T + i] = X[5 * i + 4];
     }
     for (int i = 0; i < tu; ++i) { h[5 * T + i] = U[2 * i]; h[5 * T + tu + i] = U[2 * i + 1]; }
+    // global pose of the reference line: heading integrates X[i-1,3] over ds, position the mean
+    // heading of each step (trajectory_loader.py:38-58; host libm, as numpy)
+    double* gx = h.data() + 5 * T + 2 * tu;
+    double* gy = gx + T;
+    double* gpsi = gy + T;
+    gx[0] = gy[0] = gpsi[0] = 0.0;
+    for (int i = 1; i < T; ++i) {
+        const double ds = s[i] - s[i - 1];
+        const double psi_old = gpsi[i - 1];
+        const double psi_new = psi_old + X[5 * (i - 1) + 3] * ds;
+        const double psi_avg = (psi_old + psi_new) / 2.0;
+        gpsi[i] = psi_new;
+        gx[i] = gx[i - 1] + std::cos(psi_avg) * ds;
+        gy[i] = gy[i - 1] + std::sin(psi_avg) * ds;
+    }
     mpc_ctx* c = (mpc_ctx*)std::calloc(1, sizeof(mpc_ctx));
     if (!c) return fail(MPC_E_ALLOC, "calloc");
     c->device = device;
@@ -1472,6 +1504,9 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     c->tab.v = c->table_buf + 4 * T;
     c->tab.u1 = c->table_buf + 5 * T;
     c->tab.u2 = c->table_buf + 5 * T + tu;
+    c->tab.gx = c->table_buf + 5 * T + 2 * tu;
+    c->tab.gy = c->tab.gx + T;
+    c->tab.gpsi = c->tab.gy + T;
     c->tab.T = T;
     c->tab.Tu = tu;
     c->tab.smax = s[T - 1];
@@ -1741,6 +1776,175 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
     hipStreamSynchronize(st);
     release();
     return rc;
+}
+
+extern "C" int mpc_global_pose(mpc_ctx* c, int n, const double* s, const double* d, double* out) {
+    if (!c) return fail(MPC_E_ARG, "ctx is NULL");
+    if (n < 0 || (n > 0 && (!s || !d || !out))) return fail(MPC_E_ARG, "bad global-pose arguments");
+    if (n == 0) return MPC_SUCCESS;
+    HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
+    double* buf = nullptr;
+    HIPCHK(hipMalloc(&buf, sizeof(double) * 5 * (size_t)n), MPC_E_ALLOC);
+    hipStream_t st = c->stream;
+    int rc = MPC_SUCCESS;
+    if (hipMemcpyAsync(buf, s, sizeof(double) * n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(buf + n, d, sizeof(double) * n, hipMemcpyHostToDevice, st) != hipSuccess) {
+        rc = fail(MPC_E_DEVICE, "hipMemcpy global pose inputs");
+    } else {
+        hipLaunchKernelGGL(mpc_pose_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c->tab, n, buf, buf + n, buf + 2 * n);
+        if (hipGetLastError() != hipSuccess) rc = fail(MPC_E_LAUNCH, "global pose kernel");
+        else if (hipMemcpyAsync(out, buf + 2 * n, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                 hipStreamSynchronize(st) != hipSuccess)
+            rc = fail(MPC_E_DEVICE, "hipMemcpy global pose");
+    }
+    hipStreamSynchronize(st);
+    hipFree(buf);
+    return rc;
+}
+
+// ------------------------------------------------------------------------------------------
+// trajectory JSON (the reference's format: {"X": [[s,d,o,k,v], ...], "U": [[u1,u2], ...], ...},
+// trajectory_loader.py:13-24); a small recursive-descent reader, host only
+// ------------------------------------------------------------------------------------------
+namespace {
+struct JsonReader {
+    const char* p;
+    const char* end;
+    std::string err;
+    void ws() { while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p; }
+    bool expect(char ch) {
+        ws();
+        if (p < end && *p == ch) { ++p; return true; }
+        err = std::string("expected '") + ch + "'";
+        return false;
+    }
+    bool string(std::string* out) {
+        if (!expect('"')) return false;
+        std::string r;
+        while (p < end && *p != '"') {
+            if (*p == '\\' && p + 1 < end) { r.push_back(p[1]); p += 2; }
+            else r.push_back(*p++);
+        }
+        if (p >= end) { err = "unterminated string"; return false; }
+        ++p;
+        if (out) *out = r;
+        return true;
+    }
+    bool number(double* out) {
+        ws();
+        char* e = nullptr;
+        double v = std::strtod(p, &e);
+        if (e == p) { err = "expected a number"; return false; }
+        p = e;
+        *out = v;
+        return true;
+    }
+    bool skip() {   // any value
+        ws();
+        if (p >= end) { err = "unexpected end"; return false; }
+        if (*p == '"') return string(nullptr);
+        if (*p == '{' || *p == '[') {
+            const char open = *p, close = open == '{' ? '}' : ']';
+            ++p;
+            ws();
+            if (p < end && *p == close) { ++p; return true; }
+            while (true) {
+                if (open == '{') { if (!string(nullptr) || !expect(':')) return false; }
+                if (!skip()) return false;
+                ws();
+                if (p < end && *p == ',') { ++p; continue; }
+                return expect(close);
+            }
+        }
+        if (!std::strncmp(p, "true", 4)) { p += 4; return true; }
+        if (!std::strncmp(p, "false", 5)) { p += 5; return true; }
+        if (!std::strncmp(p, "null", 4)) { p += 4; return true; }
+        double v;
+        return number(&v);
+    }
+    // [[a, b, ...], ...] with rows of exactly `width` numbers
+    bool matrix(int width, std::vector<double>* out, int* rows) {
+        if (!expect('[')) return false;
+        *rows = 0;
+        ws();
+        if (p < end && *p == ']') { ++p; return true; }
+        while (true) {
+            if (!expect('[')) return false;
+            for (int j = 0; j < width; ++j) {
+                double v;
+                if (!number(&v)) return false;
+                out->push_back(v);
+                if (j + 1 < width && !expect(',')) {
+                    err = "row of the wrong width (expected " + std::to_string(width) + " numbers)";
+                    return false;
+                }
+            }
+            if (!expect(']')) {
+                err = "row of the wrong width (expected " + std::to_string(width) + " numbers)";
+                return false;
+            }
+            ++*rows;
+            ws();
+            if (p < end && *p == ',') { ++p; continue; }
+            return expect(']');
+        }
+    }
+};
+}  // namespace
+
+extern "C" int mpc_read_trajectory_json(const char* path, double* X, int maxT, double* U, int maxTu, int* T,
+                                        int* Tu) {
+    if (!path || !T || !Tu) return fail(MPC_E_ARG, "path, T and Tu are required");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(MPC_E_ARG, std::string("File not found : ") + path + ".");   // trajectory_loader.py:18
+    std::string text;
+    char chunk[65536];
+    size_t got;
+    while ((got = std::fread(chunk, 1, sizeof(chunk), f)) > 0) text.append(chunk, got);
+    std::fclose(f);
+    JsonReader r{text.data(), text.data() + text.size(), ""};
+    std::vector<double> xs, us;
+    int tx = -1, tu = -1;
+    bool ok = r.expect('{');
+    r.ws();
+    if (ok && r.p < r.end && *r.p == '}') ok = false, r.err = "empty object";
+    while (ok) {
+        std::string key;
+        ok = r.string(&key) && r.expect(':');
+        if (!ok) break;
+        if (key == "X") ok = r.matrix(5, &xs, &tx);
+        else if (key == "U") ok = r.matrix(2, &us, &tu);
+        else ok = r.skip();
+        if (!ok) break;
+        r.ws();
+        if (r.p < r.end && *r.p == ',') { ++r.p; continue; }
+        ok = r.expect('}');
+        break;
+    }
+    if (!ok) return fail(MPC_E_ARG, std::string("trajectory JSON: ") + r.err + " at byte " +
+                                        std::to_string((long)(r.p - text.data())));
+    if (tx < 0 || tu < 0) return fail(MPC_E_ARG, "trajectory JSON: missing 'X' or 'U'");
+    *T = tx;
+    *Tu = tu;
+    if (X) {
+        if (maxT < tx) return fail(MPC_E_ARG, "X buffer too small");
+        std::memcpy(X, xs.data(), sizeof(double) * xs.size());
+    }
+    if (U) {
+        if (maxTu < tu) return fail(MPC_E_ARG, "U buffer too small");
+        std::memcpy(U, us.data(), sizeof(double) * us.size());
+    }
+    return MPC_SUCCESS;
+}
+
+extern "C" int mpc_create_from_json(const char* path, const mpc_params* p, int device, mpc_ctx** out) {
+    int T = 0, Tu = 0;
+    int rc = mpc_read_trajectory_json(path, nullptr, 0, nullptr, 0, &T, &Tu);
+    if (rc) return rc;
+    std::vector<double> X((size_t)5 * T), U((size_t)2 * Tu);
+    rc = mpc_read_trajectory_json(path, X.data(), T, U.data(), Tu, &T, &Tu);
+    if (rc) return rc;
+    return mpc_create(X.data(), T, U.data(), Tu, p, device, out);
 }
 
 extern "C" int mpc_lookup(mpc_ctx* c, int n, const double* s, double* out_state, double* out_control) {

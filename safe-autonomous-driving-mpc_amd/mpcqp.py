@@ -50,7 +50,7 @@ class MpcError(RuntimeError):
 
 EXPORTS = ["mpc_default_params", "mpc_create", "mpc_solve_batch", "mpc_solve_batch_device", "mpc_lookup",
            "mpc_set_params", "mpc_get_params", "mpc_last_error", "mpc_version", "mpc_destroy", "mpc_default_fsm",
-           "mpc_closed_loop"]
+           "mpc_closed_loop", "mpc_global_pose", "mpc_read_trajectory_json", "mpc_create_from_json"]
 
 _lib = None
 
@@ -81,6 +81,12 @@ def lib():
     L.mpc_version.restype = C.c_int
     L.mpc_destroy.argtypes = [C.c_void_p]
     L.mpc_default_fsm.argtypes = [C.POINTER(MpcFsm)]
+    L.mpc_global_pose.restype = C.c_int
+    L.mpc_global_pose.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp]
+    L.mpc_read_trajectory_json.restype = C.c_int
+    L.mpc_read_trajectory_json.argtypes = [C.c_char_p, _dp, C.c_int, _dp, C.c_int, _ip, _ip]
+    L.mpc_create_from_json.restype = C.c_int
+    L.mpc_create_from_json.argtypes = [C.c_char_p, C.POINTER(MpcParams), C.c_int, C.POINTER(C.c_void_p)]
     L.mpc_closed_loop.restype = C.c_int
     L.mpc_closed_loop.argtypes = [C.c_void_p, C.c_int, _dp, C.POINTER(MpcFsm), C.c_int, C.c_double, _dp, _dp, _dp,
                                   _ip, _ip, _ip, _dp]
@@ -110,6 +116,18 @@ def default_fsm(**kw):
     for k, v in kw.items():
         setattr(f, k, v)
     return f
+
+
+def read_trajectory_json(path):
+    """Native reader of the reference trajectory JSON (mpc_read_trajectory_json): returns (X [T,5], U [Tu,2])."""
+    T, Tu = C.c_int(), C.c_int()
+    b = os.fsencode(path)
+    _check(lib().mpc_read_trajectory_json(b, None, 0, None, 0, C.byref(T), C.byref(Tu)), "mpc_read_trajectory_json")
+    X = np.empty((T.value, 5))
+    U = np.empty((Tu.value, 2))
+    _check(lib().mpc_read_trajectory_json(b, X.ctypes.data_as(_dp), T.value, U.ctypes.data_as(_dp), Tu.value,
+                                          C.byref(T), C.byref(Tu)), "mpc_read_trajectory_json")
+    return X, U
 
 
 def _p(a):
@@ -198,6 +216,16 @@ class Solver:
                                      float(s_stop), _p(hx), _p(hu), _p(ho), _pi(ht), _pi(hs), _pi(ns), _p(sm)),
                "mpc_closed_loop")
         return dict(hist_x=hx, hist_u=hu, hist_obs_s=ho, hist_tl=ht, hist_status=hs, n_steps=ns, step_ms=sm)
+
+    def global_pose(self, s, d):
+        """TrajectoryLoader.get_global_pose on the device table, batched: s, d [n] -> [n, 3] (x, y, psi)."""
+        s = np.ascontiguousarray(s, np.float64).ravel()
+        d = np.ascontiguousarray(d, np.float64).ravel()
+        if s.shape != d.shape:
+            raise ValueError("s and d must have the same length")
+        out = np.empty((s.size, 3))
+        _check(lib().mpc_global_pose(self.h, s.size, _p(s), _p(d), _p(out)), "mpc_global_pose")
+        return out
 
     def lookup(self, s):
         s = np.ascontiguousarray(s, np.float64).ravel()

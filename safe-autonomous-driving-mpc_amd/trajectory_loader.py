@@ -45,6 +45,17 @@ class TrajectoryLoader:
         self.s_values = s
         self._limit = min(len(s), len(self.U_ref))       # :73-75
         self.s_max = s[-1]
+        # global geometry of the reference line (:32-62): heading integrates X[i-1,3] over ds, position
+        # the mean heading of each step
+        gx, gy, gpsi = [0.0], [0.0], [0.0]
+        for i in range(1, len(s)):
+            ds = s[i] - s[i - 1]
+            psi_new = gpsi[-1] + self.X_ref[i - 1, 3] * ds
+            psi_avg = (gpsi[-1] + psi_new) / 2.0
+            gpsi.append(psi_new)
+            gx.append(gx[-1] + np.cos(psi_avg) * ds)
+            gy.append(gy[-1] + np.sin(psi_avg) * ds)
+        self.global_x, self.global_y, self.global_psi = np.array(gx), np.array(gy), np.array(gpsi)
 
     @staticmethod
     def _interp(x, y, v):
@@ -61,6 +72,16 @@ class TrajectoryLoader:
         x = self.s_values
         return np.array([s, float(self._interp(x, X[:, 1], s)), float(self._interp(x, X[:, 2], s)),
                          float(self._interp(x, X[:, 3], s)), float(self._interp(x, X[:, 4], s))])
+
+    def get_global_pose(self, s, d):
+        """Frenet (s, d) -> global (x, y, psi) for animation/telemetry (:104-116); s clamped to s_max."""
+        if s > self.s_max:
+            s = self.s_max
+        x = self.s_values
+        xr = float(self._interp(x, self.global_x, s))
+        yr = float(self._interp(x, self.global_y, s))
+        psi = float(self._interp(x, self.global_psi, s))
+        return np.array([xr - d * np.sin(psi), yr + d * np.cos(psi), psi])
 
     def get_control(self, s):
         """Optimal controls [u1, u2] at arclength s ([0, 0] past s_max)."""

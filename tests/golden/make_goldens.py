@@ -112,6 +112,26 @@ def gen_interp():
     save("interp_golden", **out)
 
 
+def gen_pose():
+    """TrajectoryLoader global geometry (trajectory_loader.py:32-62) and get_global_pose
+    (:104-116) on the reference's own trajectories: knots, mid-segments, s < 0, s >= s_max."""
+    out = {}
+    rng = np.random.default_rng(12)
+    for i in (1, 2, 3):
+        ld = loader(i)
+        smax = ld.s_max
+        S = np.concatenate([rng.uniform(-3.0, smax + 3.0, 250), ld.interp_d.x[:40], [smax, smax + 1.0, -1.0, 0.0]])
+        D = rng.uniform(-1.5, 1.5, S.size)
+        P = np.array([ld.get_global_pose(float(s), float(d)) for s, d in zip(S, D)])
+        out[f"t{i}_s"] = S
+        out[f"t{i}_d"] = D
+        out[f"t{i}_pose"] = P
+        out[f"t{i}_gx"] = np.asarray(ld.global_x)
+        out[f"t{i}_gy"] = np.asarray(ld.global_y)
+        out[f"t{i}_gpsi"] = np.asarray(ld.global_psi)
+    save("pose_golden", **out)
+
+
 # ----------------------------------------------------------------------------------------
 # instance generators (SURVEY 8(d))
 # ----------------------------------------------------------------------------------------
@@ -681,9 +701,9 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--quick", action="store_true")
     a = ap.parse_args()
-    todo = a.only.split(",") if a.only else ["convert", "interp", "model", "warmstart", "qpdata", "qp",
+    todo = a.only.split(",") if a.only else ["convert", "interp", "pose", "model", "warmstart", "qpdata", "qp",
                                               "solve", "closedloop"]
-    fns = dict(convert=convert_trajectories, interp=gen_interp, model=gen_model, warmstart=gen_warmstart,
+    fns = dict(convert=convert_trajectories, interp=gen_interp, pose=gen_pose, model=gen_model, warmstart=gen_warmstart,
                qpdata=gen_qpdata, qp=lambda: gen_qp(a.quick), solve=gen_solve, closedloop=gen_closedloop)
     for t in todo:
         print(f"== {t}")

@@ -122,3 +122,35 @@ def test_fsm_struct_defaults(built):
     assert TT.fsm_params(TT.ObstaclesFSM()) is None
     rc = mpcqp.lib().mpc_closed_loop(None, 1, None, None, 10, 0.0, None, None, None, None, None, None, None)
     assert rc == -1 and "ctx" in mpcqp.last_error()
+
+
+def test_native_json_reader(built, tmp_path):
+    """mpc_read_trajectory_json reads the reference's trajectory format (trajectory_loader.py:13-24)
+    exactly: written here from the bundled arrays (X, U, S, plus an unknown key), read back bit-exact."""
+    import json
+    import mpcqp
+    from conftest import traj_arrays
+    X, U = traj_arrays(2)
+    path = tmp_path / "trajectory2.json"
+    path.write_text(json.dumps({"meta": {"a": [1, 2, {"b": None}], "ok": True}, "X": X.tolist(), "U": U.tolist(),
+                                "S": list(range(len(U)))}, indent=4))
+    Xr, Ur = mpcqp.read_trajectory_json(str(path))
+    assert np.array_equal(Xr, X) and np.array_equal(Ur, U)
+    with pytest.raises(mpcqp.MpcError, match="File not found"):
+        mpcqp.read_trajectory_json(str(tmp_path / "missing.json"))
+    bad = tmp_path / "bad.json"
+    bad.write_text('{"X": [[0, 1, 2, 3]], "U": []}')
+    with pytest.raises(mpcqp.MpcError, match="wrong width"):
+        mpcqp.read_trajectory_json(str(bad))
+
+
+def test_host_global_pose_matches_reference_golden():
+    """The shim's TrajectoryLoader.get_global_pose == reference (trajectory_loader.py:104-116), bit-exact."""
+    from conftest import load_golden
+    from trajectory_loader import TrajectoryLoader, builtin_trajectory
+    g = load_golden("pose_golden")
+    for i in (1, 2, 3):
+        ld = TrajectoryLoader(builtin_trajectory(i))
+        assert np.array_equal(ld.global_x, g[f"t{i}_gx"]) and np.array_equal(ld.global_psi, g[f"t{i}_gpsi"])
+        P = np.array([ld.get_global_pose(s, d) for s, d in zip(g[f"t{i}_s"], g[f"t{i}_d"])])
+        assert np.array_equal(P, g[f"t{i}_pose"])

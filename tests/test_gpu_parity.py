@@ -281,3 +281,30 @@ def test_closed_loop_config1(lib):
     # the reference's SLSQP stops at ftol=1e-3 (trajectory_tracking.py:255), so its closed loop is an
     # inexact-solver trajectory; the lateral offsets agree to within half a metre over the whole run
     assert np.abs(hx[:m, 1] - ref_x[:m, 1]).max() < 0.5
+
+
+def test_global_pose_device_vs_golden(lib, solvers):
+    """mpc_global_pose == TrajectoryLoader.get_global_pose (trajectory_loader.py:104-116); device sin/cos
+    may differ from libm by an ulp, so 1e-9 m / rad."""
+    g = load_golden("pose_golden")
+    for i in (1, 2, 3):
+        P = solvers[i].global_pose(g[f"t{i}_s"], g[f"t{i}_d"])
+        assert np.abs(P - g[f"t{i}_pose"]).max() <= 1e-9, i
+
+
+def test_create_from_json_matches(lib, tmp_path):
+    """mpc_create_from_json on the reference's JSON format == mpc_create on the same arrays."""
+    import ctypes
+    X, U = traj_arrays(3)
+    path = tmp_path / "trajectory3.json"
+    path.write_text(json.dumps({"X": X.tolist(), "U": U.tolist()}))
+    p = lib.default_params(N=10)
+    h = ctypes.c_void_p()
+    rc = lib.lib().mpc_create_from_json(str(path).encode(), ctypes.byref(p), 0, ctypes.byref(h))
+    assert rc == 0, lib.last_error()
+    s = np.linspace(-5.0, 2000.0, 777)
+    st = np.empty((s.size, 5)); ct = np.empty((s.size, 2))
+    assert lib.lib().mpc_lookup(h, s.size, lib._p(s), lib._p(st), lib._p(ct)) == 0
+    lib.lib().mpc_destroy(h)
+    st2, ct2 = lib.Solver(X, U, p).lookup(s)
+    assert np.array_equal(st, st2) and np.array_equal(ct, ct2)

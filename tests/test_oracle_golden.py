@@ -111,3 +111,11 @@ def test_qp_solution_vs_certified_golden(oracles):
             assert r["status"] in (0, 2), (r, viol)
     assert nfeas >= 40
     print("worst |U - U*| =", worst)
+
+
+def test_global_pose_bit_exact(oracles):
+    """orc_global_pose == TrajectoryLoader.get_global_pose (trajectory_loader.py:32-62,104-116)."""
+    g = load_golden("pose_golden")
+    for i in (1, 2, 3):
+        P = np.array([oracles[i].global_pose(s, d) for s, d in zip(g[f"t{i}_s"], g[f"t{i}_d"])])
+        assert np.array_equal(P, g[f"t{i}_pose"])
