@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--closed-loop", type=int, default=0, metavar="B",
+                    help="also run B egos through the device closed loop (mpc_closed_loop, SURVEY 8(f)1) on the "
+                         "config's trajectory and FSM preset and report closed-loop ego-steps/s")
     args = ap.parse_args()
 
     import numpy as np
@@ -151,11 +154,43 @@ def main():
                                  "x B / avg launch time (HIP events on the launch stream)",
                          "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
         }
+        if args.closed_loop:
+            out["closed_loop"] = closed_loop(args.config, args.closed_loop, N, local)
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def closed_loop(config, B, N, device):
+    """B egos through run_simulation on the device (trajectory_tracking.py:377-443): starts near the
+    reference start (s0 ~ U(0,2), v0 ~ U(0.5,2)), the config's FSM preset, until every ego
+    passed s_max - 1 or 3000 steps.  Reports ego-steps/s over the whole call (FSM + solve + plant)."""
+    import numpy as np
+    import mpcqp
+    import workloads as W
+    import trajectory_tracking as TT
+    cfg = W.CONFIGS[config]
+    ld = W.loader(cfg["traj"])
+    rng = np.random.default_rng(cfg["seed"])
+    s0 = rng.uniform(0.0, 2.0, B)
+    x_init = np.array([[s, 0.0, 0.0, ld.get_state(s)[3], v] for s, v in zip(s0, rng.uniform(0.5, 2.0, B))])
+    fsm = None
+    if cfg["obstacles"] in ("fsm2", "fsm3"):
+        fsm = TT.fsm_params(TT.ObstaclesFSM(True, True, preset="trajectory2" if cfg["obstacles"] == "fsm2"
+                                            else "trajectory3"))
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N), device=device)
+    t0 = time.perf_counter()
+    r = slv.closed_loop(x_init, fsm, max_steps=3000, s_max=ld.s_max)
+    dt = time.perf_counter() - t0
+    steps = int(r["n_steps"].sum())
+    ms = r["step_ms"][np.isfinite(r["step_ms"])]
+    return {"egos": B, "ego_steps": steps, "loop_steps": int(r["n_steps"].max()), "seconds": dt,
+            "ego_steps_per_s": steps / dt, "p50_step_ms": float(np.median(ms)) if ms.size else None,
+            "finished": int((r["n_steps"] < 3000).sum()),
+            "status_counts": np.bincount(r["hist_status"][r["hist_status"] >= 0], minlength=4).tolist(),
+            "fsm": cfg["obstacles"]}
 
 
 def cpu_baseline(wb, N, mo, budget_s):

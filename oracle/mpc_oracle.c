@@ -948,6 +948,13 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters) {
             cnew = comp_after(Q, S, &D, a);
         }
         if (getenv("ORC_TRACE")) fprintf(stderr, "      aff %.3e sig %.3e alpha %.3e\n", aa, sig, a);
+        {
+            /* breakdown guard: a step whose complementarity or control direction is not finite is not
+             * taken; the current iterate goes to the polish instead (NUMERICAL unless it certifies) */
+            int fin = cnew == cnew && cnew < INFINITY;
+            for (int i = 0; i < 2 * N && fin; ++i) fin = D.du[i] == D.du[i] && fabs(D.du[i]) < INFINITY;
+            if (!fin) { status = MPC_NUMERICAL; ++it; break; }
+        }
         stall = (mu < 1e-6 && cnew > 0.9 * comp) ? stall + 1 : 0;   /* late-phase no-progress counter */
         for (int i = 0; i < 2 * N; ++i) S->du[i] += a * D.du[i];
         for (int k = 1; k <= N; ++k)

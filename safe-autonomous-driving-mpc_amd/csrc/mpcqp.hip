@@ -861,6 +861,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
             for (int j = 0; j < NBOX; ++j) pbv[j] = 0.0;
             double sig = 0.0;
+            bool breakdown = false;
 #pragma unroll 1
             for (int pass = 0; pass < 3; ++pass) {
                 // pass 0: affine predictor; 1: Mehrotra corrector; 2: plain centred direction, taken when
@@ -950,6 +951,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 if (live) {
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) ca += fma(a_try, dsb[j], sb[j]) * fma(a_try, dlb[j], lb[j]);
+                    if (!(fabs(dd0) < INFINITY && fabs(dd1) < INFINITY)) ca = NAN;   // breakdown guard input
                 }
                 ca = Q.sum(ca);
                 if (pass == 0) {
@@ -962,6 +964,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     continue;
                 }
                 if (pass == 1 && ca > comp) continue;     // safeguard: take the centred direction
+                if (!(ca < INFINITY)) {                    // breakdown guard (oracle pdip): the step is not
+                    breakdown = true;                      // taken, the current iterate goes to the polish
+                    break;
+                }
                 const double alpha = a_try;
                 stall = (mu < 1e-6 && ca > 0.9 * comp) ? stall + 1 : 0;
 #pragma unroll
@@ -985,7 +991,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             wave_sync();
             PROF(8)
             it = iter + 1;
-            if (stall >= 5) { st_here = MPC_NUMERICAL; break; }
+            if (stall >= 5 || breakdown) { st_here = MPC_NUMERICAL; break; }
         }
         total_it += it;
         // NaN guard and the infeasibility flag
