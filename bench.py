@@ -163,7 +163,7 @@ def main():
         dist.destroy_process_group()
 
 
-def closed_loop(config, B, N, device):
+def closed_loop(config, B, N, device, sqp_iters=4):
     """B egos through run_simulation on the device (trajectory_tracking.py:377-443): starts near the
     reference start (s0 ~ U(0,2), v0 ~ U(0.5,2)), the config's FSM preset, until every ego
     passed s_max - 1 or 3000 steps.  Reports ego-steps/s over the whole call (FSM + solve + plant)."""
@@ -180,7 +180,9 @@ def closed_loop(config, B, N, device):
     if cfg["obstacles"] in ("fsm2", "fsm3"):
         fsm = TT.fsm_params(TT.ObstaclesFSM(True, True, preset="trajectory2" if cfg["obstacles"] == "fsm2"
                                             else "trajectory3"))
-    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N), device=device)
+    # Gauss-Newton SQP with 4 re-linearisations: a single QP at the reference warm start can stop for
+    # good behind the slower FSM car at N >= 10; the reference's SLSQP is an NLP solver
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, sqp_iters=sqp_iters), device=device)
     t0 = time.perf_counter()
     r = slv.closed_loop(x_init, fsm, max_steps=3000, s_max=ld.s_max)
     dt = time.perf_counter() - t0
@@ -190,7 +192,8 @@ def closed_loop(config, B, N, device):
             "ego_steps_per_s": steps / dt, "p50_step_ms": float(np.median(ms)) if ms.size else None,
             "finished": int((r["n_steps"] < 3000).sum()),
             "status_counts": np.bincount(r["hist_status"][r["hist_status"] >= 0], minlength=4).tolist(),
-            "fsm": cfg["obstacles"]}
+            "fsm": cfg["obstacles"], "sqp_iters": sqp_iters, "checks": "tools/debug_cl.py runs the restated "
+            "trajectory_tracking_check on sample egos"}
 
 
 def cpu_baseline(wb, N, mo, budget_s):
