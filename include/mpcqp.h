@@ -63,7 +63,9 @@ typedef struct mpc_params {
     int sqp_iters;                  /* QP solves per call: 1 = single QP at ubar (parity gate);
                                        0 = no solve: U = ubar, Xpred = predict(x0, ubar)              */
     int max_iter;                   /* PDIP iteration cap per QP                                     */
-    int polish;                     /* 1 = active-set polish of the interior-point result (default)   */
+    int polish;                     /* 0 off; 1 active-set polish of the interior-point result;
+                                       2 (default) crossover first: the active-set solve from the
+                                       unconstrained optimum, the interior point only if it fails       */
     double tol;                     /* relative primal/dual residual tolerance                        */
     double tol_mu;                  /* absolute complementarity tolerance                             */
     double elastic_rho;             /* L1 penalty of the elastic (soft) state rows                    */

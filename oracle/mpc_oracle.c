@@ -64,7 +64,7 @@ void orc_default_params(mpc_params* p) {
     p->tol = 1e-9;
     p->tol_mu = 1e-10;
     p->elastic_rho = 1e5;
-    p->polish = 1;
+    p->polish = 2;
 }
 
 static int seg(const double* x, int n, double v);
@@ -629,7 +629,9 @@ static double max_step(const qpdat* Q, const ipm_state* S, const ipm_dir* D) {
 #define POLISH_DELTA 1e-11
 #define POLISH_REFINE 4
 #define POLISH_ROUNDS 6
-static int polish(const qpdat* Q, ipm_state* S, int* infeasible) {
+#define XO_ROUNDS 1         /* rounds of the crossover attempt before the interior point */
+/* given = 1: start from the all-inactive classification (crossover) instead of classifying S */
+static int polish_from(const qpdat* Q, ipm_state* S, int* infeasible, int given, int rounds) {
     int N = Q->N;
     double rho = Q->rho;
     static __thread ipm_fact F;
@@ -640,13 +642,13 @@ static int polish(const qpdat* Q, ipm_state* S, int* infeasible) {
     for (int k = 1; k <= N; ++k)
         for (int j = 0; j < NROW; ++j) {
             cls[k][j] = 0;
-            if (!Q->on[j]) continue;
+            if (!Q->on[j] || given) continue;
             if (S->xi[k][j] > S->nu[k][j]) cls[k][j] = 2;
             else if (S->lam[k][j] > S->s[k][j]) cls[k][j] = 1;
         }
     for (int t = 0; t < N; ++t)
-        for (int j = 0; j < NBOX; ++j) clb[t][j] = S->lb[t][j] > S->sb[t][j];
-    for (int round = 0; round < POLISH_ROUNDS; ++round) {
+        for (int j = 0; j < NBOX; ++j) clb[t][j] = given ? 0 : S->lb[t][j] > S->sb[t][j];
+    for (int round = 0; round < rounds; ++round) {
         memcpy(&T, S, sizeof(T));
         for (int k = 1; k <= N; ++k) {
             memcpy(F.Qt[k], Q->Q[k], sizeof(F.Qt[k]));
@@ -775,6 +777,8 @@ static int polish(const qpdat* Q, ipm_state* S, int* infeasible) {
     return 0;
 }
 
+static int polish(const qpdat* Q, ipm_state* S, int* infeasible) { return polish_from(Q, S, infeasible, 0, POLISH_ROUNDS); }
+
 /* total complementarity after a step of length a along D */
 static double comp_after(const qpdat* Q, const ipm_state* S, const ipm_dir* D, double a) {
     double c = 0.0;
@@ -828,6 +832,19 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters) {
     double gd[2 * MAXN], gc[2 * MAXN], ga[2 * MAXN];
     int status = MPC_MAX_ITER, it;
     int stall = 0;
+    if (p->polish >= 2) {
+        /* Crossover first: the active-set solve started from the unconstrained optimum (all rows
+         * inactive, du = 0, multipliers 0), XO_ROUNDS rounds.  When it certifies (KKT-consistent), it is
+         * the exact optimum and no interior-point iteration is needed (70% of the C2 batch). */
+        static __thread ipm_state Z;
+        memset(&Z, 0, sizeof(Z));
+        int inf = 0;
+        if (polish_from(Q, &Z, &inf, 1, XO_ROUNDS)) {
+            memcpy(S->du, Z.du, sizeof(double) * 2 * N);
+            *iters = 0;
+            return inf ? MPC_INFEASIBLE : MPC_OK;
+        }
+    }
 
     for (it = 0; it < p->max_iter; ++it) {
         rollout_lin(Q, S->du, X);

@@ -573,6 +573,7 @@ __device__ unsigned long long g_prof[16];
 #define POLISH_DELTA 1e-11
 #define POLISH_REFINE 4
 #define POLISH_ROUNDS 6
+#define XO_ROUNDS 1            // rounds of the crossover attempt before the interior point
 #define MU0 1.0
 
 // ------------------------------------------------------------------------------------------
@@ -730,29 +731,40 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         const double bscale = Q.max(bscale_l);
         wave_sync();
 
-        // ---- K4: PDIP; interior-point state of this lane's rows in registers ---------------------
+        // ---- K4: crossover, then (if it does not certify) PDIP and the polish of its iterate ------
+        // Phase 0 is the active-set solve started from the unconstrained optimum: all rows inactive,
+        // multipliers 0, du = 0 (oracle pdip(): XO_ROUNDS rounds).  When it certifies (KKT-consistent),
+        // it is the exact optimum and no interior-point iteration runs (70% of the C2 batch).
         double rs[NR], rl[NR], rxi[NR], rnu[NR], sb[NBOX], lb[NBOX];
 #pragma unroll
-        for (int j = 0; j < NR; ++j) {
-            // centred start: xi covers the violation, s*lam = MU0 with lam <= rho/2, nu = rho - lam
-            const double r0 = -bk[j];
-            const double xi = (r0 < 0 ? -r0 : 0.0) + XI0;
-            const double sv = r0 + xi;
-            const double lam = fmin(MU0 * frcp(sv), 0.5 * rho);
-            rxi[j] = xi; rs[j] = sv; rl[j] = lam; rnu[j] = rho - lam;
-        }
+        for (int j = 0; j < NR; ++j) { rs[j] = 0.0; rl[j] = 0.0; rxi[j] = 0.0; rnu[j] = 0.0; }
 #pragma unroll
-        for (int j = 0; j < NBOX; ++j) {
-            const double r0 = -bb[j];
-            sb[j] = r0 > 1.0 ? r0 : 1.0;
-            lb[j] = 1.0;
-        }
+        for (int j = 0; j < NBOX; ++j) { sb[j] = 0.0; lb[j] = 0.0; }
         int it = 0, st_here = MPC_MAX_ITER, stall = 0;
         double mu = 0.0;
         // x4: state of stage k along the current iterate, G du (du = 0 at the start); updated with the
         // state direction of every step, so the linear rollout never re-runs (it is linear in du)
         double x4[4] = {0.0, 0.0, 0.0, 0.0};
         double du0 = 0.0, du1 = 0.0;        // control k-1 of the current iterate
+        for (int phase = Pr.polish >= 2 ? 0 : 1; phase < 2; ++phase) {
+        bool accepted = false;
+        double bad = 0.0;
+        if (phase == 1) {
+    #pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                // centred start: xi covers the violation, s*lam = MU0 with lam <= rho/2, nu = rho - lam
+                const double r0 = -bk[j];
+                const double xi = (r0 < 0 ? -r0 : 0.0) + XI0;
+                const double sv = r0 + xi;
+                const double lam = fmin(MU0 * frcp(sv), 0.5 * rho);
+                rxi[j] = xi; rs[j] = sv; rl[j] = lam; rnu[j] = rho - lam;
+            }
+    #pragma unroll
+            for (int j = 0; j < NBOX; ++j) {
+                const double r0 = -bb[j];
+                sb[j] = r0 > 1.0 ? r0 : 1.0;
+                lb[j] = 1.0;
+            }
         PROF(0)
         for (int iter = 0; iter < Pr.max_iter; ++iter) {
             PROF(1)
@@ -995,7 +1007,6 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         }
         total_it += it;
         // NaN guard and the infeasibility flag
-        double bad = 0.0;
         if (live) bad = (du0 == du0 && du1 == du1) ? 0.0 : 1.0;
         bad = Q.max(bad);
         if (bad > 0.0) {
@@ -1010,8 +1021,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             if (Q.max(inf) > 0.0) st_here = MPC_INFEASIBLE;
         }
         wave_sync();
+        }   // phase 1: interior point
 
-        // ---- active-set polish (oracle polish()) --------------------------
+        // ---- active-set polish (oracle polish()) ----------------------------
         PROF(8)
         if (Pr.polish && bad == 0.0) {
             // opaque copies of the row bounds (see the interior-point loop): nothing the polish derives
@@ -1029,9 +1041,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int j = 0; j < NBOX; ++j) clb[j] = (live && lb[j] > sb[j]) ? 1 : 0;
             // the interior-point iterate (du, x4) is the start of every round and the fallback
             double pu0 = du0, pu1 = du1;
-            bool accepted = false;
             double nviol_acc = 0.0;
-            for (int round = 0; round < POLISH_ROUNDS; ++round) {
+            const int rounds = phase == 0 ? XO_ROUNDS : POLISH_ROUNDS;
+            for (int round = 0; round < rounds; ++round) {
                 double tl[NR], tlb[NBOX];
 #pragma unroll
                 for (int j = 0; j < NR; ++j) tl[j] = rl[j];
@@ -1183,6 +1195,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             }
             wave_sync();
         }
+        if (accepted || phase == 1) break;
+        }   // phases
         status = st_here;
         if (live) {
             S.ub[2 * (k - 1)] += du0;
@@ -1397,7 +1411,7 @@ extern "C" void mpc_default_params(mpc_params* p) {
     p->tol = 1e-9;
     p->tol_mu = 1e-10;
     p->elastic_rho = 1e5;
-    p->polish = 1;
+    p->polish = 2;
 }
 
 extern "C" const char* mpc_last_error(void) { return g_err.c_str(); }

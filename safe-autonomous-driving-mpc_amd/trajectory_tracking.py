@@ -55,7 +55,7 @@ class TrajectoryTracker:
         self.linearization = 1
         self.sqp_iters = 1
         self.max_iter = 80
-        self.polish = 1
+        self.polish = 2
         self.tol = 1e-9
         self.tol_mu = 1e-10
         self.elastic_rho = 1e5
