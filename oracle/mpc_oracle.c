@@ -30,9 +30,9 @@
 #define MAXN MPC_MAX_N
 #define NROW 9      /* soft one-sided rows per stage                       */
 #define NBOX 4      /* hard box rows per control stage                     */
-#define XI0 1e-4    /* initial elastic slack                                */
+#define XI0 1e-1    /* initial elastic slack                                */
 #define TAU 0.995   /* fraction to the boundary                             */
-#define MU0 1.0     /* initial complementarity of the soft rows                */
+#define MU0 10.0     /* initial complementarity of the soft rows                */
 
 struct orc_table {
     int T, Tu;

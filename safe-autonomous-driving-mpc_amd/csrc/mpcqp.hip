@@ -29,7 +29,7 @@
 #define WAVE 64
 #define NROW 9
 #define NBOX 4
-#define XI0 1e-4
+#define XI0 1e-1
 #define TAU 0.995
 
 // ------------------------------------------------------------------------------------------
@@ -574,7 +574,7 @@ __device__ unsigned long long g_prof[16];
 #define POLISH_REFINE 4
 #define POLISH_ROUNDS 6
 #define XO_ROUNDS 1            // rounds of the crossover attempt before the interior point
-#define MU0 1.0
+#define MU0 10.0
 
 // ------------------------------------------------------------------------------------------
 // the solver kernel.  A 64-lane wavefront carries G = 64 / GL MPC instances, one per aligned group
