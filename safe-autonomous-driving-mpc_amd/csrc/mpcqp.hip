@@ -590,20 +590,42 @@ __device__ unsigned long long g_prof[16];
 template <bool OBS>
 __device__ __forceinline__ constexpr int rid(int j) { return OBS ? j : (j < 6 ? j : 8); }
 
-template <int GL, bool OBS>
+// Launch modes.  MODE_FULL: crossover (polish = 2), interior point, polish, outputs -- one launch per
+// batch.  The split pair MODE_XO + MODE_IPM is the same computation in two launches: MODE_XO runs the
+// setup and the crossover for every instance, writes the outputs of the instances it certifies and
+// appends the others to a device work list; MODE_IPM then runs the interior point (and polish) on the
+// listed instances only.  Results are identical (a failed crossover leaves no state behind), but the
+// expensive instances all start at once instead of queueing behind cheap ones on the same SIMD
+// ("two-phase launch").
+#define MODE_FULL 0
+#define MODE_XO 1
+#define MODE_IPM 2
+
+template <int GL, bool OBS, int MODE>
 __global__ void __launch_bounds__(WAVE)
 mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g, const double* __restrict__ obsg,
                  const int* __restrict__ nobsg, const double* __restrict__ ubarg, double* __restrict__ u0g,
                  double* __restrict__ Ug, double* __restrict__ Xg, int* __restrict__ statusg,
-                 int* __restrict__ itersg) {
+                 int* __restrict__ itersg, int* __restrict__ wlist, int* __restrict__ wcount) {
     constexpr int G = WAVE / GL;
     constexpr int NR = OBS ? NROW : NROW - 2;    // soft rows held per lane (6, 7: obstacle rows)
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int ln = threadIdx.x;
     const int grp = ln / GL, gl = ln % GL;
-    int b = blockIdx.x * G + grp;
-    const bool bvalid = b < B;
-    if (!bvalid) b = B - 1;          // a spare group repeats the last instance; its outputs are dropped
+    int b;
+    bool bvalid;
+    if (MODE == MODE_IPM) {
+        // instances deferred by the MODE_XO launch; waves past the end of the list exit at once
+        const int cnt = *wcount;
+        if ((int)blockIdx.x * G >= cnt) return;
+        const int slot = blockIdx.x * G + grp;
+        bvalid = slot < cnt;
+        b = wlist[bvalid ? slot : cnt - 1];
+    } else {
+        b = blockIdx.x * G + grp;
+        bvalid = b < B;
+        if (!bvalid) b = B - 1;      // a spare group repeats the last instance; its outputs are dropped
+    }
     PROF_DECL
     const Grp<GL> Q{grp * GL};
     const int N = Pr.N;
@@ -661,6 +683,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 
     const int nsqp = Pr.sqp_iters < 0 ? 0 : Pr.sqp_iters;   // 0: return ubar and predict(x0, ubar)
     int status = MPC_OK, total_it = 0;
+    bool xo_ok = false;              // MODE_XO: the crossover certified this instance
     for (int sqp = 0; sqp < nsqp; ++sqp) {
         // ---- K1: nominal rollout == predict(x0, ubar), into Xr ------------------------------
         predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
@@ -746,7 +769,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         // state direction of every step, so the linear rollout never re-runs (it is linear in du)
         double x4[4] = {0.0, 0.0, 0.0, 0.0};
         double du0 = 0.0, du1 = 0.0;        // control k-1 of the current iterate
-        for (int phase = Pr.polish >= 2 ? 0 : 1; phase < 2; ++phase) {
+        // MODE_XO runs phase 0 only and MODE_IPM phase 1 only (both compile-time)
+        const int phase_lo = MODE == MODE_XO ? 0 : (MODE == MODE_IPM ? 1 : (Pr.polish >= 2 ? 0 : 1));
+        constexpr int phase_hi = MODE == MODE_XO ? 1 : 2;
+        for (int phase = phase_lo; phase < phase_hi; ++phase) {
         bool accepted = false;
         double bad = 0.0;
         if (phase == 1) {
@@ -1195,6 +1221,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             }
             wave_sync();
         }
+        if (phase == 0) xo_ok = accepted;
         if (accepted || phase == 1) break;
         }   // phases
         status = st_here;
@@ -1208,7 +1235,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------
     PROF(9)
     predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
-    if (bvalid) {
+    if (MODE == MODE_XO && !xo_ok) {
+        // not certified: defer to the MODE_IPM launch (group-uniform)
+        if (bvalid && gl == 0) wlist[atomicAdd(wcount, 1)] = b;
+    } else if (bvalid) {
         if (gl < N && Ug) {
             Ug[(size_t)b * 2 * N + 2 * gl] = S.ub[2 * gl];
             Ug[(size_t)b * 2 * N + 2 * gl + 1] = S.ub[2 * gl + 1];
@@ -1387,6 +1417,10 @@ struct mpc_ctx {
     double *ls, *lst, *lct;
     size_t cap_lookup;
     hipStream_t stream;
+    // work list of the two-phase launch: wl[0] = count, wl[1..cap_wl] = deferred instance ids
+    int* wl;
+    size_t cap_wl;
+    bool two_phase;     // MPC_TWO_PHASE=0 in the environment selects the single MODE_FULL launch
 };
 
 extern "C" void mpc_default_params(mpc_params* p) {
@@ -1508,6 +1542,10 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     if (!c) return fail(MPC_E_ALLOC, "calloc");
     c->device = device;
     c->p = *p;
+    {
+        const char* e = std::getenv("MPC_TWO_PHASE");
+        c->two_phase = !(e && e[0] == '0');
+    }
     if (hipMalloc(&c->table_buf, h.size() * sizeof(double)) != hipSuccess) {
         std::free(c);
         return fail(MPC_E_ALLOC, "hipMalloc table");
@@ -1568,6 +1606,7 @@ extern "C" void mpc_destroy(mpc_ctx* c) {
     hipStreamSynchronize(c->stream);
     free_staging(c);
     hipFree(c->ls); hipFree(c->lst); hipFree(c->lct);
+    hipFree(c->wl);
     hipFree(c->table_buf);
     hipStreamDestroy(c->stream);
     std::free(c);
@@ -1585,14 +1624,38 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     const int G = WAVE / GL;
     const size_t lds_wave = lds * G;
     const dim3 grid((B + G - 1) / G);
+    // Two-phase launch (MODE_XO then MODE_IPM) for single-QP solves with the crossover on; the work
+    // list lives in the context (one list per context: a context is not re-entrant, include/mpcqp.h).
+    const bool split = kp.polish >= 2 && kp.sqp_iters == 1 && c->two_phase;
+    if (split && (size_t)B > c->cap_wl) {
+        hipFree(c->wl);
+        c->wl = nullptr;
+        c->cap_wl = 0;
+        HIPCHK(hipMalloc(&c->wl, sizeof(int) * ((size_t)B + 1)), MPC_E_ALLOC);
+        c->cap_wl = (size_t)B;
+    }
+    int* wl = split ? c->wl + 1 : nullptr;
+    int* wcnt = split ? c->wl : nullptr;
+    if (split) HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
     // obstacle rows exist only when obstacles are passed
-#define MPC_LAUNCH(GLV, OBSV)                                                                               \
-    hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV>), grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, obs, nob, \
-                       ubar, u0, U, Xpred, status, iters)
+#define MPC_LAUNCH(GLV, OBSV, MODEV)                                                                          \
+    hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV, MODEV>), grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, x0, \
+                       obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt)
+#define MPC_LAUNCH_GL(MODEV)                                                                   \
+    do {                                                                                       \
+        if (GL == 16) { if (with_obs) MPC_LAUNCH(16, true, MODEV); else MPC_LAUNCH(16, false, MODEV); } \
+        else if (GL == 32) { if (with_obs) MPC_LAUNCH(32, true, MODEV); else MPC_LAUNCH(32, false, MODEV); } \
+        else { if (with_obs) MPC_LAUNCH(64, true, MODEV); else MPC_LAUNCH(64, false, MODEV); } \
+    } while (0)
     const bool with_obs = obs != nullptr && kp.max_obs > 0;
-    if (GL == 16) { if (with_obs) MPC_LAUNCH(16, true); else MPC_LAUNCH(16, false); }
-    else if (GL == 32) { if (with_obs) MPC_LAUNCH(32, true); else MPC_LAUNCH(32, false); }
-    else { if (with_obs) MPC_LAUNCH(64, true); else MPC_LAUNCH(64, false); }
+    if (split) {
+        MPC_LAUNCH_GL(MODE_XO);
+        HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
+        MPC_LAUNCH_GL(MODE_IPM);
+    } else {
+        MPC_LAUNCH_GL(MODE_FULL);
+    }
+#undef MPC_LAUNCH_GL
 #undef MPC_LAUNCH
     HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
     return MPC_SUCCESS;
