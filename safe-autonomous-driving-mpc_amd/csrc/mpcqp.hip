@@ -235,23 +235,49 @@ __device__ __forceinline__ double frcp(double x) {
 // ------------------------------------------------------------------------------------------
 // lane groups: IPW instances per 64-lane wavefront, GL = 64 / IPW lanes each
 // ------------------------------------------------------------------------------------------
+// Cross-lane moves of a double for the group reductions: DPP within a row of 16 lanes (quad_perm
+// xor 1 / xor 2, row_half_mirror, row_mirror; a few cycles each) and ds_swizzle xor 16 within 32 lanes,
+// instead of ds_bpermute (~80 cycles per hop).  After the quad steps every lane of a quad holds the
+// quad value, so the mirrors pair the right partners; a + b == b + a keeps all lanes bit-identical.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+__device__ __forceinline__ double swz16_d(double v) {          // lane ^ 16 within each 32-lane half
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)(unsigned)b, 0x401F);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(unsigned)(b >> 32), 0x401F);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+#define DPP_XOR1 0xB1          // quad_perm [1,0,3,2]
+#define DPP_XOR2 0x4E          // quad_perm [2,3,0,1]
+#define DPP_HMIRROR 0x141      // row_half_mirror
+#define DPP_MIRROR 0x140       // row_mirror
+
 template <int GL>
 struct Grp {
     int base;   // first lane of the group
-    __device__ __forceinline__ double sum(double v) const {
-#pragma unroll
-        for (int m = GL / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+    template <typename OP>
+    __device__ __forceinline__ double reduce(double v, OP op) const {
+        v = op(v, dpp_d<DPP_XOR1>(v));
+        v = op(v, dpp_d<DPP_XOR2>(v));
+        v = op(v, dpp_d<DPP_HMIRROR>(v));
+        v = op(v, dpp_d<DPP_MIRROR>(v));
+        if (GL >= 32) v = op(v, swz16_d(v));
+        if (GL >= 64) v = op(v, __shfl_xor(v, 32, WAVE));
         return v;
+    }
+    __device__ __forceinline__ double sum(double v) const {
+        return reduce(v, [](double a, double b) { return a + b; });
     }
     __device__ __forceinline__ double max(double v) const {
-#pragma unroll
-        for (int m = GL / 2; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, WAVE));
-        return v;
+        return reduce(v, [](double a, double b) { return fmax(a, b); });
     }
     __device__ __forceinline__ double min(double v) const {
-#pragma unroll
-        for (int m = GL / 2; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, WAVE));
-        return v;
+        return reduce(v, [](double a, double b) { return fmin(a, b); });
     }
     __device__ __forceinline__ double get(double v, int rel) const { return __shfl(v, base + rel, WAVE); }
 };
