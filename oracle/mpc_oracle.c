@@ -32,7 +32,7 @@
 #define NBOX 4      /* hard box rows per control stage                     */
 #define XI0 1e-1    /* initial elastic slack                                */
 #define TAU 0.995   /* fraction to the boundary                             */
-#define MU0 10.0     /* initial complementarity of the soft rows                */
+#define MU0 1000.0   /* initial complementarity of the soft rows                */
 
 struct orc_table {
     int T, Tu;
@@ -62,7 +62,7 @@ void orc_default_params(mpc_params* p) {
     p->sqp_iters = 1;
     p->max_iter = 80;
     p->tol = 1e-9;
-    p->tol_mu = 1e-10;
+    p->tol_mu = 1e-9;
     p->elastic_rho = 1e5;
     p->polish = 2;
 }
@@ -627,7 +627,7 @@ static double max_step(const qpdat* Q, const ipm_state* S, const ipm_dir* D) {
  * KKT-consistent (multiplier signs/caps, inactive rows satisfied, violated rows still violated);
  * otherwise the interior-point iterate stands.  Returns 1 if accepted (S->du replaced). */
 #define POLISH_DELTA 1e-11
-#define POLISH_REFINE 4
+#define POLISH_REFINE 2
 #define POLISH_ROUNDS 6
 #define XO_ROUNDS 1         /* rounds of the crossover attempt before the interior point */
 /* given = 1: start from the all-inactive classification (crossover) instead of classifying S */
@@ -818,11 +818,19 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters) {
             S->nu[k][j] = rho - lam;
             if (fabs(Q->b[k][j]) > bscale) bscale = fabs(Q->b[k][j]);
         }
+    /* box rows start on the rows' central path: sb*lb = the mean soft-row complementarity.  The elastic
+     * rows' products are of order rho (1e5); box multipliers started at 1 need ~8 short-step iterations
+     * to grow to that scale when a violated row pushes a control onto its box. */
+    double rowc = 0.0;
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < NROW; ++j)
+            if (Q->on[j]) rowc += S->s[k][j] * S->lam[k][j] + S->xi[k][j] * S->nu[k][j];
+    const double mrow = rowc / (double)(2 * nsoft * N);
     for (int t = 0; t < N; ++t)
         for (int j = 0; j < NBOX; ++j) {
             double r0 = -Q->bb[t][j];
             S->sb[t][j] = r0 > 1.0 ? r0 : 1.0;
-            S->lb[t][j] = 1.0;
+            S->lb[t][j] = mrow / S->sb[t][j];
             if (fabs(Q->bb[t][j]) > bscale) bscale = fabs(Q->bb[t][j]);
         }
     double X[MAXN + 1][5];
