@@ -151,7 +151,9 @@ def main():
                          "unit": "TFLOP/s", "frac": flops / avg_launch_s / 1e12 / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
                          "note": "FP64 compute; achieved = SURVEY 8(d) dense-condensed flop count F(N, mean iters) "
-                                 "x B / avg launch time (HIP events on the launch stream)",
+                                 "x B / avg step time (HIP events on the launch stream; a step is the path's launch "
+                                 "pair: crossover kernel + interior-point kernel on the deferred instances, "
+                                 "DESIGN.md 3); traffic = PMC HBM bytes per step (profiles/pmc_hbm_bytes.json)",
                          "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
         }
         if args.closed_loop:
