@@ -1027,28 +1027,34 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 // the corrector would not reduce complementarity (oracle: comp_after > comp)
                 const double smu = (pass >= 1) ? sig * mu : 0.0;
                 const double cw = (pass == 1) ? 1.0 : 0.0;     // weight of the second-order term
-                // reduced right-hand side per row, scaled by 1/d: wr = rh / d  (newton() of the oracle)
-                double wr[NR], wrb[NBOX];
+                // reduced right-hand side per row, scaled by 1/d: wr = rh / d  (newton() of the oracle).
+                // Recomputed after the solve rather than held live across it (register pressure).
+                auto row_wr = [&](int j) {
+                    const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
+                    const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
+                    const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
+                    const double rx = rho - rl[j] - rnu[j];
+                    const double rh = -rp - r4 * il[j] + fma(rxi[j], rx, r5) * inu[j];
+                    return ron[j] ? rh * wv[j] : 0.0;
+                };
+                auto box_wr = [&](int j) {
+                    const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
+                    const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
+                    return (-rp - r4 * ilb[j]) * wb[j];
+                };
                 {
                     double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
                     for (int j = 0; j < NR; ++j) {
-                        const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
-                        const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
-                        const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
-                        const double rx = rho - rl[j] - rnu[j];
-                        const double rh = -rp - r4 * il[j] + fma(rxi[j], rx, r5) * inu[j];
-                        wr[j] = ron[j] ? rh * wv[j] : 0.0;
+                        const double w = row_wr(j);
 #pragma unroll
                         for (int a = 0; a < 4; ++a)
-                            if (cf[j][a] != 0.0) q4[a] = fma(cf[j][a], wr[j], q4[a]);
+                            if (cf[j][a] != 0.0) q4[a] = fma(cf[j][a], w, q4[a]);
                     }
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) {
-                        const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
-                        const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
-                        wrb[j] = (-rp - r4 * ilb[j]) * wb[j];
-                        if (j < 2) g0 += bsign(j) * wrb[j]; else g1 += bsign(j) * wrb[j];
+                        const double w = box_wr(j);
+                        if (j < 2) g0 += bsign(j) * w; else g1 += bsign(j) * w;
                     }
                     if (live) {
 #pragma unroll
@@ -1073,7 +1079,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
                     const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
                     const double rx = rho - rl[j] - rnu[j];
-                    const double dl = fma(-wv[j], dot4(cf[j], dx4), wr[j]);
+                    const double dl = fma(-wv[j], dot4(cf[j], dx4), row_wr(j));
                     const double ds = -fma(rs[j], dl, r4) * il[j];
                     const double dn = rx - dl;
                     const double dxi = -fma(rxi[j], dn, r5) * inu[j];
@@ -1091,7 +1097,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j) {
                     const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
-                    const double dl = fma(-wb[j] * bsign(j), (j < 2 ? dd0 : dd1), wrb[j]);
+                    const double dl = fma(-wb[j] * bsign(j), (j < 2 ? dd0 : dd1), box_wr(j));
                     const double ds = -fma(sb[j], dl, r4) * ilb[j];
                     dsb[j] = live ? ds : 0.0;
                     dlb[j] = live ? dl : 0.0;
@@ -1284,6 +1290,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 for (int j = 0; j < NBOX; ++j)
                     if (clb[j] == 1) lmax = fmax(lmax, fabs(tlb[j]));
                 lmax = Q.max(lmax);
+                // a row is offending when its KKT condition fails (oracle polish_from: bad > 0); only the
+                // flags matter, so no division by the scales (each IEEE division is ~10 instructions)
                 double worst = 0.0, nviol = 0.0, finite = 1.0;
                 bool flip[NR], flipb[NBOX];
                 if (live && (!(pu0 == pu0) || !(pu1 == pu1))) finite = 0.0;
@@ -1293,17 +1301,17 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     if (!ron[j]) continue;
                     const double bsc = 1.0 + fabs(bkp[j]);
                     const double r = dot4(cf[j], xp) - bkp[j];
-                    double badv = 0.0;
+                    bool badv;
                     if (cls[j] == 1) {
-                        if (tl[j] < -1e-9 * lmax) badv = -tl[j] / lmax;
-                        else if (tl[j] > rho * (1.0 + 1e-9)) badv = (tl[j] - rho) / lmax;
-                        else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
+                        badv = tl[j] < -1e-9 * lmax || tl[j] > rho * (1.0 + 1e-9) || fabs(r) > 1e-7 * bsc;
                     } else if (cls[j] == 2) {
-                        if (r > 1e-9 * bsc) badv = r / bsc;
+                        badv = r > 1e-9 * bsc;
                         if (r < -1e-6 * bsc) nviol += 1.0;
-                    } else if (r < -1e-9 * bsc) badv = -r / bsc;
-                    worst = fmax(worst, badv);
-                    flip[j] = badv > 0.0;
+                    } else {
+                        badv = r < -1e-9 * bsc;
+                    }
+                    if (badv) worst = 1.0;
+                    flip[j] = badv;
                 }
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j) {
@@ -1311,13 +1319,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     if (!live) continue;
                     const double bsc = 1.0 + fabs(bbp[j]);
                     const double r = bsign(j) * (j < 2 ? pu0 : pu1) - bbp[j];
-                    double badv = 0.0;
-                    if (clb[j] == 1) {
-                        if (tlb[j] < -1e-9 * lmax) badv = -tlb[j] / lmax;
-                        else if (fabs(r) > 1e-7 * bsc) badv = fabs(r) / bsc;
-                    } else if (r < -1e-9 * bsc) badv = -r / bsc;
-                    worst = fmax(worst, badv);
-                    flipb[j] = badv > 0.0;
+                    const bool badv = clb[j] == 1 ? (tlb[j] < -1e-9 * lmax || fabs(r) > 1e-7 * bsc) : r < -1e-9 * bsc;
+                    if (badv) worst = 1.0;
+                    flipb[j] = badv;
                 }
                 worst = Q.max(worst);
                 nviol = Q.sum(nviol);
