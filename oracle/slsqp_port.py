@@ -1,0 +1,182 @@
+"""CPU restatement of the reference's own solve path: warm start + scipy SLSQP.  TEST/BENCH ONLY.
+
+This is test infrastructure (like oracle/mpc_oracle.c): only tests/ and bench.py's CPU-baseline
+legs import it.  The product path (libmpcqp) never does.
+
+It restates, statement for statement and in the same floating-point accumulation order, what
+medinammartin3/Safe-Autonomous-Driving-MPC runs per MPC step on the CPU:
+
+  TrajectoryTracker.predict      trajectory_tracking.py:87-114   explicit Euler, k_ref = X_ref.get_state(s)[3]
+  TrajectoryTracker.cost         trajectory_tracking.py:116-152  += w_d.., += w_o.., += w_v.. per stage, then += w_u1.., += w_u2..
+  TrajectoryTracker.constraints  trajectory_tracking.py:155-211  rows per stage: 6 lane, one per obstacle, v >= 0
+  TrajectoryTracker.solve        trajectory_tracking.py:213-263  sticky-brake warm start, bounds, SLSQP
+                                                                  (ftol 1e-3, maxiter 15, finite-difference gradients)
+
+The interpolation is the package's TrajectoryLoader (scipy interp1d 'linear' arithmetic, pinned
+bit-exact by tests/golden/interp_golden.npz).  scipy.optimize.minimize(method='SLSQP') is the same
+third-party solver the reference calls (scipy is importable here and on the GPU box).
+
+Pinning: tests/test_slsqp_port.py checks predict/cost/constraints against model_golden.npz, the
+warm start against warmstart_golden.npz, and the whole solve against solve_golden.npz (the
+reference's own solve() outputs captured by tests/golden/make_goldens.py: U, nit, status, fun).
+"""
+import os
+import sys
+import time
+
+import numpy as np
+from scipy.optimize import minimize
+
+_PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "safe-autonomous-driving-mpc_amd")
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+
+from trajectory_loader import TrajectoryLoader, builtin_trajectory  # noqa: E402
+
+
+class SlsqpTracker:
+    """The reference TrajectoryTracker's numerical path (same attributes and defaults, :12-47)."""
+
+    def __init__(self, X_ref, N=5):
+        self.X_ref = X_ref
+        self.dt = 0.2
+        self.N = int(N)
+        self.u_min = np.array([-0.6, -5.0])
+        self.u_max = np.array([0.6, 4.0])
+        self.vehicle_radius = 1.0
+        self.w_d, self.w_o, self.w_v = 10.0, 10.0, 5.0
+        self.w_u1, self.w_u2 = 0.5, 0.5
+        self.obstacle_safety_distance = 5.0
+        self.max_time_2_obs = 1.5
+        self.wheelbase = 2.8
+        self.lane_width = 3.0
+        self.safe_lane_margin = 0.1
+
+    def predict(self, x0, U_flat):
+        """:87-114 — x_{k+1} = x_k + dt * [v, v o, v (k - k_ref(s_k)), u1, u2]."""
+        U = np.asarray(U_flat).reshape(self.N, 2)
+        X = np.zeros((self.N + 1, 5))
+        X[0] = x0
+        x = np.array(x0, dtype=np.float64)
+        for j in range(self.N):
+            k_ref = self.X_ref.get_state(x[0])[3]
+            s, d, o, k, v = x
+            x = x + self.dt * np.array([v, v * o, v * (k - k_ref), U[j, 0], U[j, 1]])
+            X[j + 1] = x
+        return X
+
+    def cost(self, U_flat, x0):
+        """:116-152, same accumulation order (one += per term)."""
+        U = np.asarray(U_flat).reshape(self.N, 2)
+        X = self.predict(x0, U_flat)
+        c = 0.0
+        for j in range(1, self.N + 1):
+            s, d, o, _, v = X[j]
+            r = self.X_ref.get_state(s)
+            c += self.w_d * (d - r[1]) ** 2
+            c += self.w_o * (o - r[2]) ** 2
+            c += self.w_v * (v - r[4]) ** 2
+        for j in range(self.N):
+            c += self.w_u1 * U[j, 0] ** 2
+            c += self.w_u2 * U[j, 1] ** 2
+        return c
+
+    def constraints(self, x0, obstacles):
+        """:155-211 — {'type': 'ineq', 'fun': g(U) >= 0}."""
+        sl = self.lane_width / 2.0 - self.vehicle_radius - self.safe_lane_margin
+        half, full = self.wheelbase / 2.0, self.wheelbase
+
+        def g(U_flat):
+            X = self.predict(x0, U_flat)
+            out = []
+            for j in range(1, self.N + 1):
+                s, d, o, v = X[j, 0], X[j, 1], X[j, 2], X[j, 4]
+                out.append(sl - d)
+                out.append(d + sl)
+                vf = d + half * o
+                out.append(sl - vf)
+                out.append(vf + sl)
+                va = d + full * o
+                out.append(sl - va)
+                out.append(va + sl)
+                for ob in obstacles:
+                    gap = ob["s"] + ob["v"] * (j * self.dt) - s
+                    out.append(gap - max(self.obstacle_safety_distance, v * self.max_time_2_obs))
+                out.append(v)
+            return np.array(out)
+        return {"type": "ineq", "fun": g}
+
+    def warm_start(self, x0, obstacles):
+        """:224-246 — reference controls along s_k = s0 + k v0 dt; once any obstacle lies less than
+        40 m ahead of the advancing s_k the brake flag sticks (u2 = -2) for the rest of the horizon."""
+        u = []
+        s_curr, v_curr = x0[0], x0[4]
+        brake = False
+        for _ in range(self.N):
+            for ob in obstacles:
+                if (ob["s"] - s_curr) < 40.0:
+                    brake = True
+            ur = self.X_ref.get_control(s_curr)
+            u.append([ur[0], -2.0] if brake else ur)
+            s_curr += v_curr * self.dt
+        return np.array(u).ravel()
+
+    def solve(self, x0, obstacles):
+        """:213-263 -> (u0, pred_X, solve_time, scipy result)."""
+        x0 = np.asarray(x0, dtype=np.float64)
+        U0 = self.warm_start(x0, obstacles)
+        bounds = [(self.u_min[0], self.u_max[0]), (self.u_min[1], self.u_max[1])] * self.N
+        t0 = time.time()
+        r = minimize(self.cost, U0, args=(x0,), method="SLSQP", bounds=bounds,
+                     constraints=self.constraints(x0, obstacles),
+                     options={"ftol": 1e-3, "disp": False, "maxiter": 15})
+        t = time.time() - t0
+        U = r.x.reshape(self.N, 2)
+        return U[0], self.predict(x0, r.x), t, r
+
+
+def obstacle_dicts(obs, n):
+    """[M,2] slab + count -> the reference's list of {'s', 'v'} dicts."""
+    return [{"s": float(obs[i, 0]), "v": float(obs[i, 1])} for i in range(int(n))]
+
+
+# ---- bounded process-pool timing (bench.py cpu_reference leg) --------------------------------
+_W = {}
+
+
+def _init(traj, N):
+    _W["tr"] = SlsqpTracker(TrajectoryLoader(builtin_trajectory(traj)), N)
+
+
+def _solve_chunk(args):
+    x0s, obs, nob = args
+    tr = _W["tr"]
+    for b in range(x0s.shape[0]):
+        ob = [] if obs is None else obstacle_dicts(obs[b], nob[b])
+        tr.solve(x0s[b], ob)
+    return x0s.shape[0]
+
+
+def time_batch(traj, N, x0, obs=None, n_obs=None, budget_s=10.0, procs=8, chunk=2):
+    """Solve egos of the batch with the reference's SLSQP path in `procs` worker processes (one
+    ego at a time per process, like the reference's per-step loop) until `budget_s` has passed;
+    returns (solves, seconds)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    B = x0.shape[0]
+    jobs = []
+    for lo in range(0, B, chunk):
+        hi = min(B, lo + chunk)
+        jobs.append((x0[lo:hi], None if obs is None else obs[lo:hi], None if n_obs is None else n_obs[lo:hi]))
+    done = 0
+    with ctx.Pool(procs, initializer=_init, initargs=(traj, N)) as pool:
+        pool.map(_solve_chunk, [(j[0][:1], None if j[1] is None else j[1][:1], None if j[2] is None else j[2][:1])
+                                for j in jobs[:procs]], chunksize=1)   # warm the workers (imports, first calls)
+        t0 = time.perf_counter()
+        j = 0
+        while time.perf_counter() - t0 < budget_s:
+            batch = [jobs[(j + i) % len(jobs)] for i in range(procs)]
+            done += sum(pool.map(_solve_chunk, batch, chunksize=1))
+            j += procs
+        dt = time.perf_counter() - t0
+    return done, dt
