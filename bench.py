@@ -160,6 +160,7 @@ def main():
             out["closed_loop"] = closed_loop(args.config, args.closed_loop, N, local)
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
+            out["cpu_reference"] = cpu_reference(wb, N, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -221,6 +222,22 @@ def cpu_baseline(wb, N, mo, budget_s):
     return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port",
             "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by the oracle's C PDIP "
                       f"(oracle/mpc_oracle.c) with OpenMP"}
+
+
+def cpu_reference(wb, N, budget_s):
+    """The reference's own per-step solve (trajectory_tracking.py:213-263: warm start + scipy SLSQP,
+    ftol 1e-3, maxiter 15, finite-difference gradients), restated bit-exactly in oracle/slsqp_port.py
+    and run one ego at a time per host process on a bounded sample of the same egos."""
+    import slsqp_port as SP
+    procs = min(16, os.cpu_count() or 1)
+    n = min(256, wb["x0"].shape[0])
+    sl = slice(0, n)
+    done, dt = SP.time_batch(wb["traj"], N, wb["x0"][sl], None if wb["obs"] is None else wb["obs"][sl],
+                             None if wb["n_obs"] is None else wb["n_obs"][sl], budget_s=budget_s, procs=procs)
+    return {"value": done / dt, "unit": "solves/s", "cores": procs, "kind": "port",
+            "sample": f"{done} solves of the first {n} egos of the same batch in {dt:.1f} s by the reference's "
+                      f"SLSQP solve path (oracle/slsqp_port.py, pinned to the reference's solve() outputs), "
+                      f"{procs} processes"}
 
 
 if __name__ == "__main__":

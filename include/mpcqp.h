@@ -95,7 +95,8 @@ int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, cons
                     const double* ubar, double* u0, double* U, double* Xpred, int* status, int* iters);
 
 /* Same, with device pointers, launched asynchronously on `stream` (a hipStream_t; 0 = null stream).
- * No host synchronisation, no allocation (graph-capturable). */
+ * No host synchronisation, no allocation (graph-capturable): the two-phase work list is allocated
+ * by mpc_create for up to 2^20 instances; a larger B runs the single-kernel path (same results). */
 int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const double* obs, const int* n_obs,
                            const double* ubar, double* u0, double* U, double* Xpred, int* status,
                            int* iters, void* stream);

@@ -145,6 +145,8 @@ _W = {}
 
 
 def _init(traj, N):
+    import warnings
+    warnings.simplefilter("ignore", RuntimeWarning)     # scipy's "clipping to bounds" notices
     _W["tr"] = SlsqpTracker(TrajectoryLoader(builtin_trajectory(traj)), N)
 
 

@@ -1544,6 +1544,7 @@ struct mpc_ctx {
     size_t cap_lookup;
     hipStream_t stream;
     // work list of the two-phase launch: wl[0] = count, wl[1..cap_wl] = deferred instance ids
+#define MPC_WORKLIST_CAP (1 << 20)
     int* wl;
     size_t cap_wl;
     bool two_phase;     // MPC_TWO_PHASE=0 in the environment selects the single MODE_FULL launch
@@ -1700,6 +1701,15 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         std::free(c);
         return fail(MPC_E_DEVICE, "hipStreamCreate");
     }
+    // work list of the two-phase launch (count + ids), allocated here once so that no solve call
+    // allocates; without it every batch runs the single-kernel path
+    if (hipMalloc(&c->wl, sizeof(int) * ((size_t)MPC_WORKLIST_CAP + 1)) == hipSuccess) {
+        c->cap_wl = MPC_WORKLIST_CAP;
+    } else {
+        c->wl = nullptr;
+        c->cap_wl = 0;
+        (void)hipGetLastError();
+    }
     *out = c;
     return MPC_SUCCESS;
 }
@@ -1754,14 +1764,9 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     // list lives in the context (one list per context: a context is not re-entrant, include/mpcqp.h).
     // With one instance per wavefront (G = 1, N > 31) nothing is stranded behind a slower partner, and
     // the crossover rarely certifies at those horizons (C5: 9%), so the split only repeats the setup.
-    const bool split = kp.polish >= 2 && kp.sqp_iters == 1 && c->two_phase && G >= 2;
-    if (split && (size_t)B > c->cap_wl) {
-        hipFree(c->wl);
-        c->wl = nullptr;
-        c->cap_wl = 0;
-        HIPCHK(hipMalloc(&c->wl, sizeof(int) * ((size_t)B + 1)), MPC_E_ALLOC);
-        c->cap_wl = (size_t)B;
-    }
+    // The list is allocated once by mpc_create (MPC_WORKLIST_CAP ids), so this path allocates nothing
+    // and stays graph-capturable; a larger batch runs the single-kernel path (same results).
+    const bool split = kp.polish >= 2 && kp.sqp_iters == 1 && c->two_phase && G >= 2 && (size_t)B <= c->cap_wl;
     int* wl = split ? c->wl + 1 : nullptr;
     int* wcnt = split ? c->wl : nullptr;
     if (split) HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
