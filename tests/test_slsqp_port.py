@@ -49,6 +49,14 @@ def test_warm_start_bit_exact_vs_reference():
         assert np.array_equal(tr.warm_start(c["x0"], obs_list(c["obs"])), c["ubar"])
 
 
+def test_pool_timing_leg_runs():
+    """bench.py's cpu_reference leg: the bounded process-pool timing over a config's egos."""
+    import workloads as W
+    wb = W.make_batch("C1", B=4)
+    done, dt = SP.time_batch(wb["traj"], wb["N"], wb["x0"], budget_s=0.5, procs=2)
+    assert done >= 2 and dt > 0.0
+
+
 def test_solve_matches_reference_solve():
     """The whole SLSQP solve (:254-263) against the reference's own solve() outputs."""
     g = load_golden("solve_golden")
