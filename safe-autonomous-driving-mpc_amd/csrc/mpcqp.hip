@@ -1042,18 +1042,38 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
                     return (-rp - r4 * ilb[j]) * wb[j];
                 };
+                double wr[NR], wrb[NBOX];     // kept live by the obstacle-free variant only
                 {
                     double q4[4] = {0, 0, 0, 0}, g0 = 0.0, g1 = 0.0;
 #pragma unroll
                     for (int j = 0; j < NR; ++j) {
-                        const double w = row_wr(j);
+                        double w;
+                        if constexpr (OBS) {
+                            w = row_wr(j);
+                        } else {
+                            const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
+                            const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
+                            const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
+                            const double rx = rho - rl[j] - rnu[j];
+                            const double rh = -rp - r4 * il[j] + fma(rxi[j], rx, r5) * inu[j];
+                            wr[j] = ron[j] ? rh * wv[j] : 0.0;
+                            w = wr[j];
+                        }
 #pragma unroll
                         for (int a = 0; a < 4; ++a)
                             if (cf[j][a] != 0.0) q4[a] = fma(cf[j][a], w, q4[a]);
                     }
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) {
-                        const double w = box_wr(j);
+                        double w;
+                        if constexpr (OBS) {
+                            w = box_wr(j);
+                        } else {
+                            const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
+                            const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
+                            wrb[j] = (-rp - r4 * ilb[j]) * wb[j];
+                            w = wrb[j];
+                        }
                         if (j < 2) g0 += bsign(j) * w; else g1 += bsign(j) * w;
                     }
                     if (live) {
@@ -1079,7 +1099,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
                     const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
                     const double rx = rho - rl[j] - rnu[j];
-                    const double dl = fma(-wv[j], dot4(cf[j], dx4), row_wr(j));
+                    double wj;
+                    if constexpr (OBS) wj = row_wr(j); else wj = wr[j];
+                    const double dl = fma(-wv[j], dot4(cf[j], dx4), wj);
                     const double ds = -fma(rs[j], dl, r4) * il[j];
                     const double dn = rx - dl;
                     const double dxi = -fma(rxi[j], dn, r5) * inu[j];
@@ -1097,7 +1119,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j) {
                     const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
-                    const double dl = fma(-wb[j] * bsign(j), (j < 2 ? dd0 : dd1), box_wr(j));
+                    double wj;
+                    if constexpr (OBS) wj = box_wr(j); else wj = wrb[j];
+                    const double dl = fma(-wb[j] * bsign(j), (j < 2 ? dd0 : dd1), wj);
                     const double ds = -fma(sb[j], dl, r4) * ilb[j];
                     dsb[j] = live ? ds : 0.0;
                     dlb[j] = live ? dl : 0.0;
