@@ -85,8 +85,9 @@ int mpc_create(const double* X, int T, const double* U, int Tu, const mpc_params
 
 /* Batched TrajectoryTracker.solve (trajectory_tracking.py:213-263), host buffers, synchronous.
  *   x0     [B][5]              current states
- *   obs    [B][max_obs][2]     (s, v) of each obstacle; may be NULL if max_obs == 0
- *   n_obs  [B]                 obstacles used per instance (<= max_obs); may be NULL
+ *   obs    [B][max_obs][2]     (s, v) of each obstacle, or NULL (no obstacles).  Passing obs with
+ *                              params.max_obs == 0 is an error (MPC_E_ARG): it would ignore them.
+ *   n_obs  [B]                 obstacles used per instance (<= max_obs); NULL = all max_obs rows
  *   ubar   [B][N][2] or NULL   linearization point; NULL = the reference warm start (:224-246)
  * outputs (any may be NULL):
  *   u0 [B][2], U [B][N][2], Xpred [B][N+1][5] (nonlinear predict(x0,U*), :261),
@@ -95,8 +96,12 @@ int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, cons
                     const double* ubar, double* u0, double* U, double* Xpred, int* status, int* iters);
 
 /* Same, with device pointers, launched asynchronously on `stream` (a hipStream_t; 0 = null stream).
- * No host synchronisation, no allocation (graph-capturable): the two-phase work list is allocated
- * by mpc_create for up to 2^20 instances; a larger B runs the single-kernel path (same results). */
+ * Same argument contract as mpc_solve_batch (n_obs NULL = all max_obs rows; obs with max_obs == 0 is
+ * MPC_E_ARG).  No host synchronisation, no allocation (graph-capturable): the two-phase work list is
+ * allocated by mpc_create for up to 2^20 instances; a larger B runs the single-kernel path (same
+ * results).  The work list belongs to the context: consecutive calls on one context are ordered on
+ * the device even when they use different streams (a call on a new stream waits for the previous
+ * call's kernels), so results never depend on the streams chosen. */
 int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const double* obs, const int* n_obs,
                            const double* ubar, double* u0, double* U, double* Xpred, int* status,
                            int* iters, void* stream);

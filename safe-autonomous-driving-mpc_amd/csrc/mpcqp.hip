@@ -363,6 +363,15 @@ __device__ __forceinline__ void lds_fence() {
     __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+// step boundary of the Riccati solves.  Experiment MPC_EXP_SOLVE: no full LDS wait (the compiler
+// waits for exactly the prefetched records it uses; the stores of the previous step stay in flight)
+__device__ __forceinline__ void solve_fence() {
+#ifdef MPC_EXP_SOLVE
+    __builtin_amdgcn_sched_barrier(0);
+#else
+    lds_fence();
+#endif
+}
 
 // Riccati factorisation of  min sum 0.5 x'Qt x + 0.5 u'Rt u,  x_{t+1} = A_t x_t + B u_t,  x_0 = 0.
 // The recursion is inherently sequential over stages; it is run group-uniformly (every lane of a
@@ -512,6 +521,22 @@ __device__ __forceinline__ void load_fwd(const Lds& S, int t, FwdBuf& F) {
 __device__ __forceinline__ void bwd_step(const Lds& S, int t, double dt, const BwdBuf& B, double p5[5], int ln) {
     const double h0 = fma(dt, p5[3], B.g[0]);
     const double h1 = fma(dt, p5[4], B.g[1]);
+#ifdef MPC_EXP_SOLVE
+    // the p recursion first: kk_t is off the dependent chain (only the forward pass reads it)
+    if (t >= 1) {
+        double pa[5];
+        applyAT(B.a, dt, p5, pa);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) pa[st4(a)] += B.q[a];
+#pragma unroll
+        for (int a = 0; a < 5; ++a) p5[a] = fma(B.K[a], h0, fma(B.K[5 + a], h1, pa[a]));
+    }
+    const double w0 = h0 * B.si[0];
+    const double w1 = (h1 - B.si[1] * w0) * B.si[2];
+    const double k1 = w1 * B.si[2];
+    const double k0 = (w0 - B.si[1] * k1) * B.si[0];
+    if (ln == 0) { S.kk[2 * t] = k0; S.kk[2 * t + 1] = k1; }
+#else
     const double w0 = h0 * B.si[0];
     const double w1 = (h1 - B.si[1] * w0) * B.si[2];
     const double k1 = w1 * B.si[2];
@@ -525,6 +550,7 @@ __device__ __forceinline__ void bwd_step(const Lds& S, int t, double dt, const B
 #pragma unroll
         for (int a = 0; a < 5; ++a) p5[a] = fma(B.K[a], h0, fma(B.K[5 + a], h1, pa[a]));
     }
+#endif
 }
 // one forward step: u_t = kk_t + K_t x_t,  x_{t+1} = A_t x_t + B u_t
 __device__ __forceinline__ void fwd_step(const Lds& S, int t, double dt, const FwdBuf& F, double x[5], int ln) {
@@ -559,7 +585,7 @@ __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int ln) {
         load_bwd(S, NT - 1, buf[0]);
 #pragma unroll
         for (int t = NT - 1; t >= 0; --t) {
-            lds_fence();
+            solve_fence();
             load_bwd(S, t >= 1 ? t - 1 : 0, buf[(NT - t) & 1]);
             sched_fence();
             bwd_step(S, t, dt, buf[(NT - 1 - t) & 1], p5, ln);
@@ -569,12 +595,12 @@ __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int ln) {
         load_bwd(S, N - 1, A);
         int t = N - 1;
         while (true) {
-            lds_fence();
+            solve_fence();
             load_bwd(S, t >= 1 ? t - 1 : 0, B);      // unconditional: keeps the LDS wait counts exact
             sched_fence();
             bwd_step(S, t, dt, A, p5, ln);
             if (--t < 0) break;
-            lds_fence();
+            solve_fence();
             load_bwd(S, t >= 1 ? t - 1 : 0, A);
             sched_fence();
             bwd_step(S, t, dt, B, p5, ln);
@@ -590,7 +616,7 @@ __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int ln) {
         load_fwd(S, 0, buf[0]);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            lds_fence();
+            solve_fence();
             load_fwd(S, t + 1 < NT ? t + 1 : t, buf[(t + 1) & 1]);
             sched_fence();
             fwd_step(S, t, dt, buf[t & 1], x, ln);
@@ -600,12 +626,12 @@ __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int ln) {
         load_fwd(S, 0, A);
         int t = 0;
         while (true) {
-            lds_fence();
+            solve_fence();
             load_fwd(S, t + 1 < N ? t + 1 : t, B);
             sched_fence();
             fwd_step(S, t, dt, A, x, ln);
             if (++t >= N) break;
-            lds_fence();
+            solve_fence();
             load_fwd(S, t + 1 < N ? t + 1 : t, A);
             sched_fence();
             fwd_step(S, t, dt, B, x, ln);
@@ -753,7 +779,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     double x0[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) x0[j] = x0g[5 * (size_t)b + j];
-    int nobs = nobsg ? nobsg[b] : 0;
+    // n_obs may be NULL with an obstacle slab: every instance then uses all max_obs rows (as the
+    // host entry mpc_solve_batch does)
+    int nobs = nobsg ? nobsg[b] : (obsg ? Pr.max_obs : 0);
     nobs = nobs < 0 ? 0 : (nobs > Pr.max_obs ? Pr.max_obs : nobs);
     const double* obs = obsg ? obsg + (size_t)b * Pr.max_obs * 2 : nullptr;
     const bool has_obs = nobs > 0;
@@ -1572,6 +1600,11 @@ struct mpc_ctx {
     int* wl;
     size_t cap_wl;
     bool two_phase;     // MPC_TWO_PHASE=0 in the environment selects the single MODE_FULL launch
+    // the work list is reused by every call: a call on a different stream than the previous one
+    // first waits for the previous call's last kernel (wl_done, recorded after each split launch)
+    hipEvent_t wl_done;
+    hipStream_t wl_stream;
+    bool wl_pending;
 };
 
 extern "C" void mpc_default_params(mpc_params* p) {
@@ -1727,9 +1760,11 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     }
     // work list of the two-phase launch (count + ids), allocated here once so that no solve call
     // allocates; without it every batch runs the single-kernel path
-    if (hipMalloc(&c->wl, sizeof(int) * ((size_t)MPC_WORKLIST_CAP + 1)) == hipSuccess) {
+    if (hipMalloc(&c->wl, sizeof(int) * ((size_t)MPC_WORKLIST_CAP + 1)) == hipSuccess &&
+        hipEventCreateWithFlags(&c->wl_done, hipEventDisableTiming) == hipSuccess) {
         c->cap_wl = MPC_WORKLIST_CAP;
     } else {
+        hipFree(c->wl);
         c->wl = nullptr;
         c->cap_wl = 0;
         (void)hipGetLastError();
@@ -1766,6 +1801,7 @@ extern "C" void mpc_destroy(mpc_ctx* c) {
     hipStreamSynchronize(c->stream);
     free_staging(c);
     hipFree(c->ls); hipFree(c->lst); hipFree(c->lct);
+    if (c->wl) hipEventDestroy(c->wl_done);
     hipFree(c->wl);
     hipFree(c->table_buf);
     hipStreamDestroy(c->stream);
@@ -1793,7 +1829,11 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     const bool split = kp.polish >= 2 && kp.sqp_iters == 1 && c->two_phase && G >= 2 && (size_t)B <= c->cap_wl;
     int* wl = split ? c->wl + 1 : nullptr;
     int* wcnt = split ? c->wl : nullptr;
-    if (split) HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
+    if (split) {
+        // the previous split launch may still be reading the list on another stream: order after it
+        if (c->wl_pending && c->wl_stream != st) HIPCHK(hipStreamWaitEvent(st, c->wl_done, 0), MPC_E_DEVICE);
+        HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
+    }
     // obstacle rows exist only when obstacles are passed
 #define MPC_LAUNCH(GLV, OBSV, MODEV, NTV)                                                                   \
     hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV, MODEV, NTV>), grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, \
@@ -1811,6 +1851,10 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
         MPC_LAUNCH_GL(MODE_XO);
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
         MPC_LAUNCH_GL(MODE_IPM);
+        HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
+        HIPCHK(hipEventRecord(c->wl_done, st), MPC_E_DEVICE);
+        c->wl_stream = st;
+        c->wl_pending = true;
     } else {
         MPC_LAUNCH_GL(MODE_FULL);
     }
@@ -1828,6 +1872,8 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
     if (B == 0) return MPC_SUCCESS;
     if (!x0) return fail(MPC_E_ARG, "x0 is NULL");
     if (c->p.max_obs > 0 && n_obs && !obs) return fail(MPC_E_ARG, "n_obs given but obs is NULL");
+    if (obs && c->p.max_obs == 0)
+        return fail(MPC_E_ARG, "obs given but params.max_obs == 0 (the obstacles would be ignored)");
     int rc = check_params(&c->p);
     if (rc) return rc;
     KParams kp = kparams(&c->p);
@@ -1854,6 +1900,7 @@ extern "C" int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
     const int N = c->p.N, mo = c->p.max_obs;
+    if (obs && mo == 0) return fail(MPC_E_ARG, "obs given but params.max_obs == 0 (the obstacles would be ignored)");
     if ((size_t)B > c->cap_B || N > c->cap_N || mo > c->cap_obs) {
         size_t nb = (size_t)B > c->cap_B ? (size_t)B : c->cap_B;
         int nn = N > c->cap_N ? N : c->cap_N;
@@ -1872,16 +1919,10 @@ extern "C" int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double
     const bool use_obs = mo > 0 && obs;
     if (use_obs) {
         HIPCHK(hipMemcpyAsync(c->obs, obs, sizeof(double) * 2 * mo * B, hipMemcpyHostToDevice, s), MPC_E_DEVICE);
-        if (n_obs) {
-            HIPCHK(hipMemcpyAsync(c->nobs, n_obs, sizeof(int) * B, hipMemcpyHostToDevice, s), MPC_E_DEVICE);
-        } else {
-            std::vector<int> full(B, mo);
-            HIPCHK(hipMemcpyAsync(c->nobs, full.data(), sizeof(int) * B, hipMemcpyHostToDevice, s), MPC_E_DEVICE);
-            HIPCHK(hipStreamSynchronize(s), MPC_E_DEVICE);
-        }
+        if (n_obs) HIPCHK(hipMemcpyAsync(c->nobs, n_obs, sizeof(int) * B, hipMemcpyHostToDevice, s), MPC_E_DEVICE);
     }
     if (ubar) HIPCHK(hipMemcpyAsync(c->ub, ubar, sizeof(double) * 2 * N * B, hipMemcpyHostToDevice, s), MPC_E_DEVICE);
-    rc = mpc_solve_batch_device(c, B, c->x0, use_obs ? c->obs : nullptr, use_obs ? c->nobs : nullptr,
+    rc = mpc_solve_batch_device(c, B, c->x0, use_obs ? c->obs : nullptr, use_obs && n_obs ? c->nobs : nullptr,
                                 ubar ? c->ub : nullptr, c->u0, c->U, c->X, c->status, c->iters, (void*)s);
     if (rc) return rc;
     if (u0) HIPCHK(hipMemcpyAsync(u0, c->u0, sizeof(double) * 2 * B, hipMemcpyDeviceToHost, s), MPC_E_DEVICE);

@@ -179,6 +179,9 @@ class Solver:
         N, mo = p.N, p.max_obs
         x0 = np.ascontiguousarray(x0, np.float64).reshape(-1, 5)
         B = x0.shape[0]
+        if obs is not None and np.asarray(obs).size > 0 and mo == 0:
+            # the library refuses this too (MPC_E_ARG): an obstacle slab must never be dropped silently
+            raise ValueError("obstacles given but params.max_obs == 0: set max_obs to the slab width")
         if obs is not None and mo > 0:
             obs = np.ascontiguousarray(obs, np.float64).reshape(B, mo, 2)
             n_obs = (np.full(B, mo, np.int32) if n_obs is None

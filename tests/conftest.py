@@ -23,6 +23,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X GPU (HIP device)")
 
 
+def pytest_collection_finish(session):
+    """GPU runs: load torch's HIP runtime before libmpcqp.so is loaded.  Both carry the soname
+    libamdhip64.so.7; whichever loads first serves the process, and torch cannot initialise on the
+    system runtime that libmpcqp would pull in (bench.py imports torch first for the same reason).
+    libmpcqp itself works on either."""
+    if any(item.get_closest_marker("gpu") for item in session.items):
+        try:
+            import torch
+            torch.cuda.is_available()
+        except ImportError:
+            pass
+
+
 def load_golden(name):
     """Load tests/golden/<name>.npz (allow_pickle=False) into a dict of arrays."""
     with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:

@@ -1,0 +1,140 @@
+"""GPU tests of the device-pointer entry mpc_solve_batch_device (the path bench.py times) and of the
+launch schedule: the two-phase launch (crossover kernel + interior-point kernel on a device work
+list) must give bit-identical results to the single-kernel launch (MPC_TWO_PHASE=0), through the
+host entry and the device entry, with and without obstacles.  Also the argument contract the two
+entries share (include/mpcqp.h): n_obs NULL = every max_obs row is used; obstacles with
+max_obs == 0 are refused instead of being dropped."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import traj_arrays
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__ as g
+    g.build()
+    import mpcqp
+    return mpcqp
+
+
+def make_solver(lib, traj, N, mo, two_phase=True):
+    old = os.environ.get("MPC_TWO_PHASE")
+    os.environ["MPC_TWO_PHASE"] = "1" if two_phase else "0"
+    try:
+        return lib.Solver(*traj_arrays(traj), lib.default_params(N=N, max_obs=mo), device=0)
+    finally:
+        if old is None:
+            del os.environ["MPC_TWO_PHASE"]
+        else:
+            os.environ["MPC_TWO_PHASE"] = old
+
+
+def device_solve(slv, wb, torch, stream=None, pass_nobs=True):
+    """One mpc_solve_batch_device call on torch device buffers; returns host copies of the outputs."""
+    dev = torch.device("cuda", 0)
+    B, N = wb["x0"].shape[0], wb["N"]
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    x0 = t(wb["x0"])
+    obs = t(wb["obs"]) if wb["obs"] is not None else None
+    nob = t(wb["n_obs"], torch.int32) if (wb["n_obs"] is not None and pass_nobs) else None
+    out = dict(u0=torch.empty((B, 2), dtype=torch.float64, device=dev),
+               U=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+               Xpred=torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev),
+               status=torch.empty(B, dtype=torch.int32, device=dev),
+               iters=torch.empty(B, dtype=torch.int32, device=dev))
+    ptr = lambda x: 0 if x is None else x.data_ptr()
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    st.wait_stream(torch.cuda.current_stream(dev))      # the input copies ran on the current stream
+    slv.solve_batch_device(B, ptr(x0), ptr(obs), ptr(nob), 0, ptr(out["u0"]), ptr(out["U"]), ptr(out["Xpred"]),
+                           ptr(out["status"]), ptr(out["iters"]), stream=st.cuda_stream)
+    return out, (x0, obs, nob)
+
+
+def to_host(out, torch):
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def assert_identical(a, b, what):
+    for k in ("u0", "U", "Xpred", "status", "iters"):
+        assert np.array_equal(a[k], b[k]), (what, k, np.flatnonzero((a[k] != b[k]).reshape(len(a[k]), -1).any(1))[:8])
+
+
+@pytest.mark.parametrize("cfg,B", [("C2", 1024), ("C3", 1024)])
+def test_two_phase_equals_single_kernel(lib, cfg, B):
+    """Split launch (MODE_XO + MODE_IPM) == single launch (MODE_FULL), host and device entries."""
+    torch = pytest.importorskip("torch")
+    import workloads as W
+    wb = W.make_batch(cfg, B=B, seed=7)
+    two = make_solver(lib, wb["traj"], wb["N"], wb["max_obs"], two_phase=True)
+    one = make_solver(lib, wb["traj"], wb["N"], wb["max_obs"], two_phase=False)
+    r2 = two.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
+    r1 = one.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
+    assert_identical(r2, r1, "host entry")
+    # the batch exercises both kernels of the split launch
+    assert (r2["iters"] == 0).any() and (r2["iters"] > 0).any()
+    d2, _ = device_solve(two, wb, torch)
+    d1, _ = device_solve(one, wb, torch)
+    d2, d1 = to_host(d2, torch), to_host(d1, torch)
+    assert_identical(d2, d1, "device entry")
+    assert_identical(d2, r2, "device vs host entry")
+
+
+def test_device_entry_nobs_null_uses_all_rows(lib):
+    """Device entry with obs and n_obs == NULL == host entry with n_obs = max_obs for every instance."""
+    torch = pytest.importorskip("torch")
+    import workloads as W
+    wb = W.make_batch("C5", B=64, seed=11)
+    assert wb["max_obs"] == 8 and (wb["n_obs"] == 8).all()
+    slv = make_solver(lib, wb["traj"], wb["N"], wb["max_obs"])
+    rh = slv.solve_batch(wb["x0"], wb["obs"], np.full(64, 8, np.int32))
+    rd, _ = device_solve(slv, wb, torch, pass_nobs=False)
+    rd = to_host(rd, torch)
+    assert_identical(rd, rh, "n_obs NULL")
+    # and the obstacles really are used: without them the answers differ
+    r0 = slv.solve_batch(wb["x0"])
+    assert not np.array_equal(r0["U"], rh["U"])
+
+
+def test_device_calls_on_two_streams_are_ordered(lib):
+    """Back-to-back device calls on one context from two streams share the context's work list; the
+    second call must wait for the first (include/mpcqp.h), so both equal their host-entry results."""
+    torch = pytest.importorskip("torch")
+    import workloads as W
+    wa = W.make_batch("C3", B=2048, seed=21)
+    wb = W.make_batch("C3", B=2048, seed=22)
+    slv = make_solver(lib, wa["traj"], wa["N"], wa["max_obs"])
+    ra = slv.solve_batch(wa["x0"], wa["obs"], wa["n_obs"])
+    rb = slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
+    dev = torch.device("cuda", 0)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    for _ in range(3):
+        oa, keep_a = device_solve(slv, wa, torch, stream=s1)
+        ob, keep_b = device_solve(slv, wb, torch, stream=s2)
+        ha, hb = to_host(oa, torch), to_host(ob, torch)
+        assert_identical(ha, ra, "stream 1")
+        assert_identical(hb, rb, "stream 2")
+
+
+def test_obstacles_with_max_obs_zero_are_refused(lib):
+    """Obstacles passed while params.max_obs == 0 are an error (Python ValueError, C MPC_E_ARG), never
+    an unconstrained solve."""
+    torch = pytest.importorskip("torch")
+    import workloads as W
+    wb = W.make_batch("C3", B=8, seed=3)
+    slv = make_solver(lib, wb["traj"], wb["N"], 0)
+    with pytest.raises(ValueError):
+        slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
+    with pytest.raises(lib.MpcError):
+        device_solve(slv, wb, torch)
+    # the host C entry refuses it too
+    B = 8
+    x0 = np.ascontiguousarray(wb["x0"])
+    obs = np.ascontiguousarray(wb["obs"])
+    rc = lib.lib().mpc_solve_batch(slv.h, B, lib._p(x0), lib._p(obs), None, None, None, None, None, None, None)
+    assert rc == -1 and "max_obs" in lib.last_error()
