@@ -26,6 +26,15 @@ def algorithmic_flops(N, K):
     return 20 * N ** 2 + 24 * N ** 3 + K * (48 * N ** 3 + 8 * N ** 3 / 3 + 64 * N ** 2)
 
 
+def riccati_flops(N, K):
+    """Useful FP64 flops of the algorithm the kernel actually runs (stage-wise Riccati form),
+    per solve: setup + crossover (one factorisation, two solves) + K interior-point iterations (one
+    factorisation, two solves and the row phases each).  Per stage: factorisation 230, solve 84, row
+    phases 450 (FMA = 2); the redundant and idle lanes of the SIMD implementation are not counted."""
+    fac, sol, rows = 230, 84, 450
+    return N * (fac + 2 * sol + 60) + K * N * (fac + 2 * sol + rows)
+
+
 def algorithmic_bytes(N, max_obs):
     """x0 40 + obstacles 16*max_obs + n_obs 4 ; u0 16 + U 16N + pred_X 40(N+1) + status/iters 8."""
     return 40 + 16 * max_obs + (4 if max_obs else 0) + 16 + 16 * N + 40 * (N + 1) + 8
@@ -119,6 +128,7 @@ def main():
     kmean = tel["mean_iters"]
     avg_launch_s = gpu_s / args.steps
     flops = algorithmic_flops(N, kmean) * B
+    rflops = riccati_flops(N, kmean) * B
     nbytes = algorithmic_bytes(N, mo) * B
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_hbm_bytes.json")
@@ -150,10 +160,21 @@ def main():
             "roofline": {"bound": "mfma", "achieved": flops / avg_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / avg_launch_s / 1e12 / FP64_PEAK_TFLOPS,
                          "traffic": traffic,
-                         "note": "FP64 compute; achieved = SURVEY 8(d) dense-condensed flop count F(N, mean iters) "
-                                 "x B / avg step time (HIP events on the launch stream; a step is the path's launch "
-                                 "pair: crossover kernel + interior-point kernel on the deferred instances, "
-                                 "DESIGN.md 3); traffic = PMC HBM bytes per step (profiles/pmc_hbm_bytes.json)",
+                         "compute_unit": "FP64 VALU: the kernel issues no MFMA instructions; 'mfma' names the "
+                                         "compute roof, and MI355X's FP64 vector and FP64 matrix peaks are the "
+                                         "same 78.6 TFLOP/s",
+                         "achieved_basis": "SURVEY 8(d) flop count of a dense condensed PDIP (24N^3 per Hessian, "
+                                           "48N^3 per iteration), F(N, mean iters) x B / avg step time; this is an "
+                                           "equivalent dense-QP rate, not executed work",
+                         "riccati_TFLOPs": rflops / avg_launch_s / 1e12,
+                         "riccati_note": "useful flops of the stage-wise Riccati algorithm that runs (bench."
+                                         "riccati_flops), the same time base",
+                         "limiter": "latency of the slowest interior-point instance: the deferred instances fill "
+                                    "fewer waves than the chip has SIMDs, so the batch time is one wave's FP64 "
+                                    "issue time over its iterations (DESIGN.md 4)",
+                         "note": "HIP events on the launch stream; a step is the path's launch pair: crossover "
+                                 "kernel + interior-point kernel on the deferred instances (DESIGN.md 3); traffic = "
+                                 "PMC HBM bytes per step (profiles/pmc_hbm_bytes.json)",
                          "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
         }
         if args.closed_loop:

@@ -27,6 +27,9 @@
 #include "../../include/mpcqp.h"
 
 #define WAVE 64
+#ifndef MPC_NO_NT20
+#define MPC_NO_NT20 0
+#endif
 #define NROW 9
 #define NBOX 4
 #define XI0 1e-1
@@ -132,33 +135,44 @@ __device__ void get_control(const DevTable& t, double s, double* out) {
 // ------------------------------------------------------------------------------------------
 // Stage records read by the recursions are padded to an even number of doubles and every array
 // starts 16-B aligned, so each pair is one ds_read_b128 (4 LDS cycles) instead of a ds_read2_b64 (8).
-#define A5S 6          // stride of A5 (5 used)
+// The Riccati recursions are lane-distributed (section "distributed recursions" below): lane i = 0..4
+// of a group holds row i of P / component i of the state, so the records they read per lane are laid
+// out by row: QR (row i of the stage Hessian), QH (component i of the linear term), KP (column i of K).
+#define A5S 8          // stride of A5: a12, a14, a20, a23, a24, dt, 0, 0 (the zeros and dt serve the
+                       // per-lane coefficient gathers of the distributed recursions)
 #define SIS 4          // stride of Si (3 used)
+#define QRS 20         // stride of QR: rows i = 0..4 (s,d,o,k,v) x columns (s,d,o,v); row 3 (k) zero
+#define QHS 6          // stride of QH: (s,d,o,k,v) with k = 0, one pad
 struct Lds {
-    double* A5;    // [N][A5S]  a12,a14,a20,a23,a24 of A_k = I + J'_k  (a04 = dt)
+    double* A5;    // [N][A5S]
     double* cst;   // [N+1][6]  cost data of stage k: (-d_ref', -o_ref', -v_ref') and the residuals r_d, r_o, r_v
-    double* Qt;    // [N+1][10] Riccati stage Hessians on (s,d,o,v) (barrier / penalty augmented), packed
+    double* QR;    // [N+1][QRS] Riccati stage Hessians (barrier / penalty augmented), by row
     double* Rt;    // [N][2]
-    double* Kf;    // [N][10]   Riccati gains K_t (2x5)
+    double* KP;    // [N][10]   Riccati gains by column: (K(0,i), K(1,i)), i = 0..4
     double* Si;    // [N][SIS]  (1/l00, l10, 1/l11) of S_t = Ls Ls'
-    double* qh;    // [N+1][4]  LQR stage linear terms (state)
+    double* QH;    // [N+1][QHS] LQR stage linear terms (state)
     double* gh;    // [N][2]    LQR stage linear terms (control)
     double* kk;    // [N][2]
-    double* Xr;    // [N+1][5]  rollout of the current iterate
+    double* Xr;    // [N+1][5]  nominal rollout (setup, outputs); aliases QH, which is dead then
     double* dX;    // [N+1][5]  rollout of the direction
     double* dud;   // [N][2]    direction dU
-    double* yc;    // [N+1][4]  dual-residual stage terms: cost part
-    double* ya;    // [N+1][4]  dual-residual stage terms: multiplier part
-    double* zc;    // [N][2]
-    double* za;    // [N][2]
+    double* ys;    // [N+1][4]  dual-residual stage terms yc + ya (cost part + multiplier part)
+    double* zs;    // [N][2]    control terms zc + za
     double* ub;    // [N][2]    linearisation point
-    double* kap;   // [N+1]     k_ref(xbar_k); then shat_k (min obstacle prediction)
+    double* kap;   // [N+1]     k_ref(xbar_k) (setup); aliases QH after Xr
 };
+// At convergence the separate dual-residual terms (yc, ya, zc, za) go to a scratch in QR rows 0..2
+// (the factorisation is dead then; the polish rewrites those rows): yc of stage k at QR[k][0..3],
+// ya at QR[k][4..7], zc / za of control t at QR[t][8..9] / QR[t][10..11].
+#define DQ_YC 0
+#define DQ_YA 4
+#define DQ_ZC 8
+#define DQ_ZA 10
 
 __host__ __device__ inline int lds_doubles(int N) {
     int NP = N + 1;
-    int n = N * A5S + NP * 6 + NP * 10 + N * 2 + N * 10 + N * SIS + NP * 4 + N * 2 + N * 2 + N * 2 + NP * 4 +
-            NP * 4 + N * 2 + N * 2 + N * 2 + NP * 5 + NP * 5 + NP;
+    int n = N * A5S + NP * 6 + NP * QRS + N * 2 + N * 10 + N * SIS + NP * QHS + N * 2 + N * 2 + N * 2 + NP * 4 +
+            N * 2 + N * 2 + NP * 5;
     return (n + 1) & ~1;     // groups stay 16-B aligned
 }
 
@@ -168,22 +182,21 @@ __device__ inline Lds carve(double* p, int N) {
     // even-sized arrays first (16-B aligned starts), the odd-sized ones last
     L.A5 = p; p += N * A5S;
     L.cst = p; p += NP * 6;
-    L.Qt = p; p += NP * 10;
+    L.QR = p; p += NP * QRS;
     L.Rt = p; p += N * 2;
-    L.Kf = p; p += N * 10;
+    L.KP = p; p += N * 10;
     L.Si = p; p += N * SIS;
-    L.qh = p; p += NP * 4;
+    L.QH = p;
+    L.Xr = p;                 // Xr [NP][5] and kap [NP] share QH's NP * 6 doubles
+    L.kap = p + NP * 5;
+    p += NP * QHS;
     L.gh = p; p += N * 2;
     L.kk = p; p += N * 2;
     L.dud = p; p += N * 2;
-    L.yc = p; p += NP * 4;
-    L.ya = p; p += NP * 4;
-    L.zc = p; p += N * 2;
-    L.za = p; p += N * 2;
+    L.ys = p; p += NP * 4;
+    L.zs = p; p += N * 2;
     L.ub = p; p += N * 2;
-    L.Xr = p; p += NP * 5;
     L.dX = p; p += NP * 5;
-    L.kap = p; p += NP;
     return L;
 }
 
@@ -355,286 +368,362 @@ __device__ __forceinline__ void ld_a5(const double* p, double a[5]) {
     ld2(p + 4, a[4], pad);
 }
 // Software pipeline of the stage recursions: every step starts with a full LDS wait (the data of
-// this step, prefetched one step earlier, and the previous step's stores), then issues the next
-// step's loads, then computes.  The sched barriers keep the compiler from sinking the prefetch to the
-// end of the step (where the next wait would expose its whole latency) or hoisting it above the wait.
+// this step, prefetched one step earlier), then issues the next step's loads, then computes.  The
+// sched barriers keep the compiler from sinking the prefetch to the end of the step (where the next
+// wait would expose its whole latency) or hoisting it above the wait.
 __device__ __forceinline__ void lds_fence() {
     __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0), vmcnt/expcnt untouched
     __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
-// step boundary of the Riccati solves.  Experiment MPC_EXP_SOLVE: no full LDS wait (the compiler
-// waits for exactly the prefetched records it uses; the stores of the previous step stay in flight)
-__device__ __forceinline__ void solve_fence() {
-#ifdef MPC_EXP_SOLVE
-    __builtin_amdgcn_sched_barrier(0);
+
+// ------------------------------------------------------------------------------------------
+// distributed recursions.  The Riccati factorisation and solves run on lanes i = 0..4 of each
+// lane group: lane i holds row i of P (factorisation), component i of the co-state p (backward
+// solve) and of the state direction x (forward solve).  Every cross-lane term is a
+// v_fmac_f64_dpp with row_newbcast:l, i.e. a broadcast of lane l's register within its 16-lane row
+// fused into the FMA (same issue cost as a plain v_fmac_f64 on gfx950).  Compared with running the
+// whole 5x5 recursion redundantly on every lane, a stage costs ~90 instead of ~210 VALU
+// instructions.  The other lanes of the group compute discarded values (their per-lane records are
+// clamped to lane 4's; their stores are masked off).  Groups are aligned to 16-lane rows, so the
+// broadcasts never cross groups.
+// ------------------------------------------------------------------------------------------
+// dst += src@L * c  (src broadcast from lane L of each 16-lane row); asm operand lists are written
+// with early-clobber accumulators, so no accumulator shares a register with a source.  The leading
+// s_nop 1 covers the VALU-write -> DPP-read hazard (2 wait states) of the sources.
+#define DPPF(d, s, c, L) "v_fmac_f64_dpp " d ", " s ", " c " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+
+// branch-free masked LDS stores: exec is narrowed to `mask` (wave-uniform lane mask) inside one asm
+// statement, so the compiler sees straight-line code (no basic-block split around the store) and can
+// interleave the producing chain with the rest of the step.  The compiler does not count these LDS
+// ops in its lgkmcnt bookkeeping, which only makes its own waits more conservative; every reader of
+// these records runs after them in program order on the same wave (LDS returns in order).
+// s_and_saveexec writes SCC, hence the "scc" clobber (a loop condition held in SCC across the store
+// would otherwise be lost).
+__device__ __forceinline__ unsigned lds_off(const double* p) { return (unsigned)(size_t)p; }
+#ifdef MPC_NO_MST
+__device__ __forceinline__ void mst1(unsigned long long mask, const double* p, double v) {
+    if ((mask >> __lane_id()) & 1ull) *const_cast<double*>(p) = v;
+}
+__device__ __forceinline__ void mst2(unsigned long long mask, const double* p, double v0, double v1) {
+    if ((mask >> __lane_id()) & 1ull) { const_cast<double*>(p)[0] = v0; const_cast<double*>(p)[1] = v1; }
+}
 #else
-    lds_fence();
+__device__ __forceinline__ void mst1(unsigned long long mask, const double* p, double v) {
+    unsigned long long tmp;
+    asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b64 %2, %3\n\ts_mov_b64 exec, %0"
+                 : "=&s"(tmp) : "s"(mask), "v"(lds_off(p)), "v"(v) : "memory", "scc");
+}
+__device__ __forceinline__ void mst2(unsigned long long mask, const double* p, double v0, double v1) {
+    unsigned long long tmp;
+    asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write2_b64 %2, %3, %4 offset1:1\n\ts_mov_b64 exec, %0"
+                 : "=&s"(tmp) : "s"(mask), "v"(lds_off(p)), "v"(v0), "v"(v1) : "memory", "scc");
+}
 #endif
+
+// Per-lane constants of the distributed recursions.  A_t = I + J'_t with J' nonzero in rows 0..2 only:
+// J'(0,4) = dt, J'(1,2) = a12, J'(1,4) = a14, J'(2,0) = a20, J'(2,3) = a23, J'(2,4) = a24.  Lane i needs
+// e_l(i) = J'(l,i) (column i; backward recursions) and f_m(i) = J'(i,m) (row i; forward solve).  Both
+// are gathered per lane from the stage's A5 record (a12, a14, a20, a23, a24, dt, 0, 0): oXX is the
+// record offset a lane reads (6 = a zero slot).
+struct DLane {
+    int i;                     // row / component of this lane (clamped to 4 for lanes >= 5)
+    int oe1, oe2, of0, of2, of3, of4;
+    double e0;                 // J'(0,i) = dt for i = 4 (constant)
+    double bu0, bu1;           // B(i,:) = dt e3 / dt e4
+    double k0, k1, k2, k3;     // symmetrisation: lane keeps its own P(i,j) when i <= j
+    double r1, r2, r3, r4;     // lane is row 1, 2, 3, 4
+    unsigned long long m5, m0; // lanes i < 5 of every group / lane 0 of every group
+};
+__device__ __forceinline__ DLane dlane(int gl, double dt) {
+    DLane D;
+    D.i = gl < 5 ? gl : 4;
+    const int z = 6;
+    D.oe1 = gl == 2 ? 0 : (gl == 4 ? 1 : z);
+    D.oe2 = gl == 0 ? 2 : (gl == 3 ? 3 : (gl == 4 ? 4 : z));
+    D.of0 = gl == 2 ? 2 : z;
+    D.of2 = gl == 1 ? 0 : z;
+    D.of3 = gl == 2 ? 3 : z;
+    D.of4 = gl == 0 ? 5 : (gl == 1 ? 1 : (gl == 2 ? 4 : z));
+    D.e0 = gl == 4 ? dt : 0.0;
+    D.bu0 = gl == 3 ? dt : 0.0;
+    D.bu1 = gl == 4 ? dt : 0.0;
+    D.k0 = gl <= 0 ? 1.0 : 0.0;
+    D.k1 = gl <= 1 ? 1.0 : 0.0;
+    D.k2 = gl <= 2 ? 1.0 : 0.0;
+    D.k3 = gl <= 3 ? 1.0 : 0.0;
+    D.r1 = gl == 1 ? 1.0 : 0.0;
+    D.r2 = gl == 2 ? 1.0 : 0.0;
+    D.r3 = gl == 3 ? 1.0 : 0.0;
+    D.r4 = gl == 4 ? 1.0 : 0.0;
+    D.m5 = __ballot(gl < 5);
+    D.m0 = __ballot(gl == 0);
+    return D;
 }
 
 // Riccati factorisation of  min sum 0.5 x'Qt x + 0.5 u'Rt u,  x_{t+1} = A_t x_t + B u_t,  x_0 = 0.
-// The recursion is inherently sequential over stages; it is run group-uniformly (every lane of a
-// group holds the same P in registers, so no cross-lane traffic sits on the critical path), with the
-// next stage's A_t, Rt and Qt prefetched from LDS one step ahead.  Per stage: M = P A,
-// S = Rt + B'P B = Ls Ls', W = Ls^-1 B'M, K = -Ls^-T W, P <- Qt + A'M - W'W (upper triangle).  The
-// Cholesky form keeps ~2 more digits than an explicit S^-1 once barrier weights reach 1e12
-// (DESIGN.md section 3).  dt is folded into the Cholesky reciprocals and W'W into the fma chains of
-// the P update (~160 FP64 ops per stage).  The K/Si stores of a stage are issued after the next
-// stage's wait, so no wait is spent on them.
-// Restates riccati_factor() of oracle/mpc_oracle.c.
-struct FacBuf { double a[5], r0, r1, q[10]; };
-struct FacOut { double K[10], si[3]; };
-__device__ __forceinline__ void load_fac(const Lds& S, int t, FacBuf& F) {
-    ld_a5(S.A5 + A5S * t, F.a);
+// Per stage: S = Rt + B'P B = Ls Ls', M = P A, W = Ls^-1 B'M, K = -Ls^-T W, P <- A'M - W'W + Qt.  The
+// Cholesky form keeps ~2 more digits than an explicit S^-1 once barrier weights reach 1e12 (DESIGN.md
+// section 3); Qt is added last for the same reason (adding it before the cancellation A'M - W'W would
+// round that difference at Qt's magnitude).  Lane i: row i of M locally; the W terms from M(3,i),
+// M(4,i); row i of A'M and of W'W by broadcasts.  Restates riccati_factor() of oracle/mpc_oracle.c.
+struct FacRec { double a[5], r0, r1, e1, e2, q[4]; };
+__device__ __forceinline__ void load_fac(const Lds& S, const DLane& L, int t, FacRec& F) {
+    const double* a5 = S.A5 + A5S * t;
+    ld_a5(a5, F.a);
     ld2(S.Rt + 2 * t, F.r0, F.r1);
-#pragma unroll
-    for (int a = 0; a < 10; a += 2) ld2(S.Qt + 10 * t + a, F.q[a], F.q[a + 1]);
+    F.e1 = a5[L.oe1];
+    F.e2 = a5[L.oe2];
+    ld2(S.QR + QRS * t + 4 * L.i, F.q[0], F.q[1]);
+    ld2(S.QR + QRS * t + 4 * L.i + 2, F.q[2], F.q[3]);
 }
-__device__ __forceinline__ void store_fac(const Lds& S, int t, const FacOut& O, int ln) {
-    if (ln == 0) {
-#pragma unroll
-        for (int j = 0; j < 10; ++j) S.Kf[10 * t + j] = O.K[j];
-        S.Si[SIS * t] = O.si[0];
-        S.Si[SIS * t + 1] = O.si[1];
-        S.Si[SIS * t + 2] = O.si[2];
-    }
-}
-__device__ __forceinline__ void fac_step(int t, double dt, double dt2, const FacBuf& F, double P[15], FacOut& O) {
+__device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bool upd, double dt, double dt2,
+                                         const FacRec& F, double pr[5]) {
     const double a12 = F.a[0], a14 = F.a[1], a20 = F.a[2], a23 = F.a[3], a24 = F.a[4];
-    const double* q = F.q;
-    // S = Rt + dt^2 P[{3,4},{3,4}] and its Cholesky factor
-    double s00 = fma(dt2, P[s5(3, 3)], F.r0), s01 = dt2 * P[s5(3, 4)], s11 = fma(dt2, P[s5(4, 4)], F.r1);
+    // S = Rt + dt^2 P[{3,4},{3,4}]: P(3,3), P(3,4) from lane 3, P(4,4) from lane 4
+    double s00 = F.r0, s01 = 0.0, s11 = F.r1;
+    asm("s_nop 1\n\t" DPPF("%0", "%3", "%5", 3) DPPF("%1", "%4", "%5", 3) DPPF("%2", "%4", "%5", 4)
+        : "+&v"(s00), "+&v"(s01), "+&v"(s11) : "v"(pr[3]), "v"(pr[4]), "v"(dt2));
     if (!(s00 > 0.0)) s00 = 1e-300 + fabs(s00);
     const double il00 = frsqrt(s00), l10 = s01 * il00;
     double r11 = s11 - l10 * l10;
     if (!(r11 > 1e-14 * s11)) r11 = 1e-14 * fabs(s11) + 1e-300;
     const double il11 = frsqrt(r11);
     const double c0 = dt * il00, c1 = dt * il11, c2 = -l10 * il11;
-    // M = P A  (A = I + J', J' sparse: a12, a14, a20, a23, a24, dt)
-    double M[5][5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const double pi0 = P[s5(i, 0)], pi1 = P[s5(i, 1)], pi2 = P[s5(i, 2)], pi3 = P[s5(i, 3)], pi4 = P[s5(i, 4)];
-        M[i][0] = fma(pi2, a20, pi0);
-        M[i][1] = pi1;
-        M[i][2] = fma(pi1, a12, pi2);
-        M[i][3] = fma(pi2, a23, pi3);
-        M[i][4] = fma(pi0, dt, fma(pi1, a14, fma(pi2, a24, pi4)));
+    // V3 = M(3,i), V4 = M(4,i) = P(i,{3,4}) + sum_l J'(l,i) P(l,{3,4})
+    double v3 = pr[3], v4 = pr[4];
+    asm("s_nop 1\n\t" DPPF("%0", "%2", "%4", 2) DPPF("%1", "%3", "%4", 2) DPPF("%0", "%2", "%5", 1)
+        DPPF("%1", "%3", "%5", 1) DPPF("%0", "%2", "%6", 0) DPPF("%1", "%3", "%6", 0)
+        : "+&v"(v3), "+&v"(v4) : "v"(pr[3]), "v"(pr[4]), "v"(F.e2), "v"(F.e1), "v"(L.e0));
+    // row i of M = P A (local)
+    double m[5];
+    m[0] = fma(pr[2], a20, pr[0]);
+    m[1] = pr[1];
+    m[2] = fma(pr[1], a12, pr[2]);
+    m[3] = fma(pr[2], a23, pr[3]);
+    m[4] = fma(pr[0], dt, fma(pr[1], a14, fma(pr[2], a24, pr[4])));
+    double am[5] = {m[0], m[1], m[2], m[3], m[4]};
+    if (upd) {
+        // row i of A'M = M(i,:) + sum_l J'(l,i) M(l,:)
+#define DPP_AM(L, c)                                                                                        \
+        asm("s_nop 1\n\t" DPPF("%0", "%5", "%10", L) DPPF("%1", "%6", "%10", L) DPPF("%2", "%7", "%10", L) \
+            DPPF("%3", "%8", "%10", L) DPPF("%4", "%9", "%10", L)                                            \
+            : "+&v"(am[0]), "+&v"(am[1]), "+&v"(am[2]), "+&v"(am[3]), "+&v"(am[4])                           \
+            : "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]), "v"(m[4]), "v"(c))
+        DPP_AM(2, F.e2);
+        DPP_AM(1, F.e1);
+        DPP_AM(0, L.e0);
+#undef DPP_AM
     }
-    // W = Ls^-1 dt M[{3,4}, :],  K = -Ls^-T W
-    double W0[5], W1[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        W0[j] = M[3][j] * c0;
-        W1[j] = fma(M[4][j], c1, c2 * W0[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-        const double K1 = -W1[j] * il11;
-        O.K[5 + j] = K1;
-        O.K[j] = -(W0[j] + l10 * K1) * il00;
-    }
-    O.si[0] = il00;
-    O.si[1] = l10;
-    O.si[2] = il11;
-    if (t >= 1) {
-        // P <- (A'M) - W'W + Qt,  (A'M)[i][j] = M[i][j] + sum_l J'[l][i] M[l][j].  Qt is added last: near
-        // the end of the interior point it carries barrier weights up to ~1e12, and adding it before
-        // the cancellation A'M - W'W would round that difference at Qt's magnitude.
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-#pragma unroll
-            for (int j = i; j < 5; ++j) {
-                double v = M[i][j];
-                if (i == 0) v = fma(a20, M[2][j], v);
-                else if (i == 2) v = fma(a12, M[1][j], v);
-                else if (i == 3) v = fma(a23, M[2][j], v);
-                else if (i == 4) v = fma(dt, M[0][j], fma(a14, M[1][j], fma(a24, M[2][j], v)));
-                v = fma(-W0[i], W0[j], fma(-W1[i], W1[j], v));
-                if (i != 3 && j != 3) v += q[p4(i == 4 ? 3 : i, j == 4 ? 3 : j)];
-                P[s5(i, j)] = v;
-            }
-    }
-}
-__device__ void riccati_factor(const Lds& S, int N, double dt, int ln) {
-    double P[15];
-#pragma unroll
-    for (int i = 0; i < 15; ++i) P[i] = 0.0;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = a; c < 4; ++c) P[s5(st4(a), st4(c))] = S.Qt[10 * N + p4(a, c)];
-    const double dt2 = dt * dt;
-    FacBuf A, B;
-    FacOut O;
-    load_fac(S, N - 1, A);
-    lds_fence();
-    load_fac(S, N >= 2 ? N - 2 : 0, B);
-    sched_fence();
-    fac_step(N - 1, dt, dt2, A, P, O);
-    int t = N - 2;
-    while (t >= 0) {
-        lds_fence();
-        store_fac(S, t + 1, O, ln);
-        load_fac(S, t >= 1 ? t - 1 : 0, A);
-        sched_fence();
-        fac_step(t, dt, dt2, B, P, O);
-        if (--t < 0) break;
-        lds_fence();
-        store_fac(S, t + 1, O, ln);
-        load_fac(S, t >= 1 ? t - 1 : 0, B);
-        sched_fence();
-        fac_step(t, dt, dt2, A, P, O);
-        --t;
-    }
-    store_fac(S, 0, O, ln);
-    wave_sync();
-}
-
-// LQR solve with the factorisation: linear terms -qh (stages 1..N), -gh (controls).
-// Writes dud (controls) and dX (states, x_0 = 0).  Group-uniform; the stage data of the next step is
-// loaded into the other of two register buffers while the current step computes (ping-pong, so the
-// LDS latency hides behind the dependent FP64 chain); lane 0 of the group writes.
-// Restates riccati_solve() of oracle/mpc_oracle.c.
-struct BwdBuf { double g[2], si[3], a[5], K[10], q[4]; };
-struct FwdBuf { double kk[2], K[10], a[5]; };
-
-__device__ __forceinline__ void load_bwd(const Lds& S, int t, BwdBuf& B) {
-    double pad;
-    ld2(S.gh + 2 * t, B.g[0], B.g[1]);
-    ld2(S.Si + SIS * t, B.si[0], B.si[1]);
-    ld2(S.Si + SIS * t + 2, B.si[2], pad);
-    ld_a5(S.A5 + A5S * t, B.a);
-#pragma unroll
-    for (int a = 0; a < 10; a += 2) ld2(S.Kf + 10 * t + a, B.K[a], B.K[a + 1]);
-    ld2(S.qh + 4 * t, B.q[0], B.q[1]);
-    ld2(S.qh + 4 * t + 2, B.q[2], B.q[3]);
-}
-__device__ __forceinline__ void load_fwd(const Lds& S, int t, FwdBuf& F) {
-    ld2(S.kk + 2 * t, F.kk[0], F.kk[1]);
-#pragma unroll
-    for (int a = 0; a < 10; a += 2) ld2(S.Kf + 10 * t + a, F.K[a], F.K[a + 1]);
-    ld_a5(S.A5 + A5S * t, F.a);
-}
-// one backward step: p <- A_t'p + K_t'h + qh_t  (t >= 1), kk_t = S_t^-1 h,  h = gh_t + B'p
-__device__ __forceinline__ void bwd_step(const Lds& S, int t, double dt, const BwdBuf& B, double p5[5], int ln) {
-    const double h0 = fma(dt, p5[3], B.g[0]);
-    const double h1 = fma(dt, p5[4], B.g[1]);
-#ifdef MPC_EXP_SOLVE
-    // the p recursion first: kk_t is off the dependent chain (only the forward pass reads it)
-    if (t >= 1) {
-        double pa[5];
-        applyAT(B.a, dt, p5, pa);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) pa[st4(a)] += B.q[a];
-#pragma unroll
-        for (int a = 0; a < 5; ++a) p5[a] = fma(B.K[a], h0, fma(B.K[5 + a], h1, pa[a]));
-    }
-    const double w0 = h0 * B.si[0];
-    const double w1 = (h1 - B.si[1] * w0) * B.si[2];
-    const double k1 = w1 * B.si[2];
-    const double k0 = (w0 - B.si[1] * k1) * B.si[0];
-    if (ln == 0) { S.kk[2 * t] = k0; S.kk[2 * t + 1] = k1; }
-#else
-    const double w0 = h0 * B.si[0];
-    const double w1 = (h1 - B.si[1] * w0) * B.si[2];
-    const double k1 = w1 * B.si[2];
-    const double k0 = (w0 - B.si[1] * k1) * B.si[0];
-    if (ln == 0) { S.kk[2 * t] = k0; S.kk[2 * t + 1] = k1; }
-    if (t >= 1) {
-        double pa[5];
-        applyAT(B.a, dt, p5, pa);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) pa[st4(a)] += B.q[a];
-#pragma unroll
-        for (int a = 0; a < 5; ++a) p5[a] = fma(B.K[a], h0, fma(B.K[5 + a], h1, pa[a]));
-    }
-#endif
-}
-// one forward step: u_t = kk_t + K_t x_t,  x_{t+1} = A_t x_t + B u_t
-__device__ __forceinline__ void fwd_step(const Lds& S, int t, double dt, const FwdBuf& F, double x[5], int ln) {
-    double v0 = fma(F.K[0], x[0], fma(F.K[1], x[1], F.kk[0]));
-    double v1 = fma(F.K[5], x[0], fma(F.K[6], x[1], F.kk[1]));
-    v0 = fma(F.K[2], x[2], v0) + fma(F.K[3], x[3], F.K[4] * x[4]);
-    v1 = fma(F.K[7], x[2], v1) + fma(F.K[8], x[3], F.K[9] * x[4]);
-    double y[5];
-    applyA(F.a, dt, x, y);
-    y[3] = fma(dt, v0, y[3]);
-    y[4] = fma(dt, v1, y[4]);
-#pragma unroll
-    for (int a = 0; a < 5; ++a) x[a] = y[a];
-    if (ln == 0) {
-        S.dud[2 * t] = v0;
-        S.dud[2 * t + 1] = v1;
-#pragma unroll
-        for (int a = 0; a < 5; ++a) S.dX[5 * (t + 1) + a] = y[a];
+    const double w0 = c0 * v3;
+    const double w1 = fma(c1, v4, c2 * w0);
+    const double K1 = -w1 * il11;
+    const double K0 = -(w0 + l10 * K1) * il00;
+    mst2(L.m5, S.KP + 10 * t + 2 * L.i, K0, K1);
+    mst2(L.m0, S.Si + SIS * t, il00, l10);
+    mst1(L.m0, S.Si + SIS * t + 2, il11);
+    if (upd) {
+        // P(i,j) = A'M(i,j) - W1_i W1_j - W0_i W0_j + Qt(i,j)
+        const double nw0 = -w0, nw1 = -w1;
+        asm("s_nop 1\n\t" DPPF("%0", "%5", "%7", 0) DPPF("%1", "%5", "%7", 1) DPPF("%2", "%5", "%7", 2)
+            DPPF("%3", "%5", "%7", 3) DPPF("%4", "%5", "%7", 4) DPPF("%0", "%6", "%8", 0) DPPF("%1", "%6", "%8", 1)
+            DPPF("%2", "%6", "%8", 2) DPPF("%3", "%6", "%8", 3) DPPF("%4", "%6", "%8", 4)
+            : "+&v"(am[0]), "+&v"(am[1]), "+&v"(am[2]), "+&v"(am[3]), "+&v"(am[4])
+            : "v"(w1), "v"(w0), "v"(nw1), "v"(nw0));
+        pr[0] = am[0] + F.q[0];
+        pr[1] = am[1] + F.q[1];
+        pr[2] = am[2] + F.q[2];
+        pr[3] = am[3];
+        pr[4] = am[4] + F.q[3];
+        // symmetrise: lane i takes P(j,i) from row j for j < i, so P is exactly symmetric (the upper
+        // triangle is the reference, as in the oracle's packed recursion).  Lane-computed lower entries
+        // differ by rounding, and with barrier weights near 1e12 that asymmetry costs interior-point
+        // iterations on hard elastic instances.
+        double sy0 = pr[0] * L.k0, sy1 = pr[1] * L.k1, sy2 = pr[2] * L.k2, sy3 = pr[3] * L.k3;
+        asm("s_nop 1\n\t" DPPF("%0", "%4", "%8", 0) DPPF("%1", "%5", "%9", 1) DPPF("%2", "%6", "%10", 2)
+            DPPF("%3", "%7", "%11", 3) DPPF("%0", "%5", "%9", 0) DPPF("%1", "%6", "%10", 1) DPPF("%2", "%7", "%11", 2)
+            DPPF("%0", "%6", "%10", 0) DPPF("%1", "%7", "%11", 1) DPPF("%0", "%7", "%11", 0)
+            : "+&v"(sy0), "+&v"(sy1), "+&v"(sy2), "+&v"(sy3)
+            : "v"(pr[1]), "v"(pr[2]), "v"(pr[3]), "v"(pr[4]), "v"(L.r1), "v"(L.r2), "v"(L.r3), "v"(L.r4));
+        pr[0] = sy0;
+        pr[1] = sy1;
+        pr[2] = sy2;
+        pr[3] = sy3;
     }
 }
-
-// NT > 0: the horizon is a compile-time constant and both passes are fully unrolled (no loop control,
-// immediate LDS offsets, no address arithmetic per step; ~20% fewer cycles per step on gfx950).
+// NT > 0: horizon fixed at compile time, stages fully unrolled (immediate LDS offsets, no loop control)
 template <int NT>
-__device__ void riccati_solve(const Lds& S, int Nrt, double dt, int ln) {
+__device__ void riccati_factor(const Lds& S, int Nrt, double dt, int gl) {
     const int N = NT > 0 ? NT : Nrt;
-    double p5[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-    for (int a = 0; a < 4; ++a) p5[st4(a)] = S.qh[4 * N + a];
+    const DLane L = dlane(gl, dt);
+    const double dt2 = dt * dt;
+    double pr[5];
+    ld2(S.QR + QRS * N + 4 * L.i, pr[0], pr[1]);
+    ld2(S.QR + QRS * N + 4 * L.i + 2, pr[2], pr[4]);
+    pr[3] = 0.0;
+#ifdef MPC_FAC_LOOP
+    if constexpr (false) {
+#else
     if constexpr (NT > 0) {
-        BwdBuf buf[2];
-        load_bwd(S, NT - 1, buf[0]);
+#endif
+        FacRec buf[2];
+        load_fac(S, L, NT - 1, buf[0]);
 #pragma unroll
         for (int t = NT - 1; t >= 0; --t) {
-            solve_fence();
-            load_bwd(S, t >= 1 ? t - 1 : 0, buf[(NT - t) & 1]);
+            lds_fence();
+            load_fac(S, L, t >= 1 ? t - 1 : 0, buf[(NT - t) & 1]);
             sched_fence();
-            bwd_step(S, t, dt, buf[(NT - 1 - t) & 1], p5, ln);
+            fac_step(S, L, t, t >= 1, dt, dt2, buf[(NT - 1 - t) & 1], pr);
         }
     } else {
-        BwdBuf A, B;
-        load_bwd(S, N - 1, A);
+        FacRec A, B;
+        load_fac(S, L, N - 1, A);
         int t = N - 1;
         while (true) {
-            solve_fence();
-            load_bwd(S, t >= 1 ? t - 1 : 0, B);      // unconditional: keeps the LDS wait counts exact
+            lds_fence();
+            load_fac(S, L, t >= 1 ? t - 1 : 0, B);      // unconditional: keeps the LDS wait counts exact
             sched_fence();
-            bwd_step(S, t, dt, A, p5, ln);
+            fac_step(S, L, t, t >= 1, dt, dt2, A, pr);
             if (--t < 0) break;
-            solve_fence();
-            load_bwd(S, t >= 1 ? t - 1 : 0, A);
+            lds_fence();
+            load_fac(S, L, t >= 1 ? t - 1 : 0, A);
             sched_fence();
-            bwd_step(S, t, dt, B, p5, ln);
+            fac_step(S, L, t, t >= 1, dt, dt2, B, pr);
             if (--t < 0) break;
         }
     }
     wave_sync();
-    if (ln == 0)
-        for (int a = 0; a < 5; ++a) S.dX[a] = 0.0;
-    double x[5] = {0, 0, 0, 0, 0};
-    if constexpr (NT > 0) {
-        FwdBuf buf[2];
-        load_fwd(S, 0, buf[0]);
+}
+
+// LQR solve with the factorisation: linear terms -QH (stages 1..N), -gh (controls).  Writes dud
+// (controls) and dX (states, x_0 = 0).  Backward: p_t = A_t'p + QH_t + K_t'h, h = gh_t + B'p,
+// kk_t = S_t^-1 h (lane i holds p_i); forward: u_t = kk_t + K_t x, x <- A_t x + B u (lane i holds x_i).
+// Restates riccati_solve() of oracle/mpc_oracle.c.
+struct BwdRec { double g0, g1, si0, si1, si2, e1, e2, K0, K1, qi; };
+struct FwdRec { double kk0, kk1, K[10], f0, f2, f3, f4; };
+__device__ __forceinline__ void load_bwd(const Lds& S, const DLane& L, int t, BwdRec& B) {
+    double pad;
+    const double* a5 = S.A5 + A5S * t;
+    ld2(S.gh + 2 * t, B.g0, B.g1);
+    ld2(S.Si + SIS * t, B.si0, B.si1);
+    ld2(S.Si + SIS * t + 2, B.si2, pad);
+    B.e1 = a5[L.oe1];
+    B.e2 = a5[L.oe2];
+    ld2(S.KP + 10 * t + 2 * L.i, B.K0, B.K1);
+    B.qi = S.QH[QHS * t + L.i];
+}
+__device__ __forceinline__ void load_fwd(const Lds& S, const DLane& L, int t, FwdRec& F) {
+    const double* a5 = S.A5 + A5S * t;
+    ld2(S.kk + 2 * t, F.kk0, F.kk1);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            solve_fence();
-            load_fwd(S, t + 1 < NT ? t + 1 : t, buf[(t + 1) & 1]);
+    for (int a = 0; a < 10; a += 2) ld2(S.KP + 10 * t + a, F.K[a], F.K[a + 1]);
+    F.f0 = a5[L.of0];
+    F.f2 = a5[L.of2];
+    F.f3 = a5[L.of3];
+    F.f4 = a5[L.of4];
+}
+__device__ __forceinline__ void bwd_step(const Lds& S, const DLane& L, int t, double dt, const BwdRec& B, double& p) {
+    double h0 = B.g0, h1 = B.g1, pn = p;
+    asm("s_nop 1\n\t" DPPF("%0", "%3", "%4", 3) DPPF("%1", "%3", "%4", 4) DPPF("%2", "%3", "%5", 2)
+        DPPF("%2", "%3", "%6", 1) DPPF("%2", "%3", "%7", 0)
+        : "+&v"(h0), "+&v"(h1), "+&v"(pn) : "v"(p), "v"(dt), "v"(B.e2), "v"(B.e1), "v"(L.e0));
+    if (t >= 1) p = fma(B.K0, h0, fma(B.K1, h1, pn + B.qi));
+    const double w0 = h0 * B.si0;
+    const double w1 = (h1 - B.si1 * w0) * B.si2;
+    const double k1 = w1 * B.si2;
+    const double k0 = (w0 - B.si1 * k1) * B.si0;
+    mst2(L.m0, S.kk + 2 * t, k0, k1);
+}
+__device__ __forceinline__ void fwd_step(const Lds& S, const DLane& L, int t, const FwdRec& F, double& x) {
+    // u = (K(:,2) x2 + (K(:,0) x0 + (K(:,1) x1 + kk))) + (K(:,3) x3 + K(:,4) x4) and x' = x + J'x with the
+    // terms in the order of the group-uniform recursion (applyA), so the solve rounds as the oracle's
+    double u0 = F.kk0, u1 = F.kk1, v0 = 0.0, v1 = 0.0, xn = x;
+    // operands: %5 x; %6..%15 = (K(0,m), K(1,m)) for m = 0..4; %16..%19 = f0, f2, f3, f4
+    asm("s_nop 1\n\t" DPPF("%0", "%5", "%8", 1) DPPF("%1", "%5", "%9", 1) DPPF("%2", "%5", "%14", 4)
+        DPPF("%3", "%5", "%15", 4) DPPF("%4", "%5", "%19", 4) DPPF("%0", "%5", "%6", 0) DPPF("%1", "%5", "%7", 0)
+        DPPF("%2", "%5", "%12", 3) DPPF("%3", "%5", "%13", 3) DPPF("%4", "%5", "%18", 3)
+        DPPF("%0", "%5", "%10", 2) DPPF("%1", "%5", "%11", 2) DPPF("%4", "%5", "%17", 2)
+        DPPF("%4", "%5", "%16", 0)
+        : "+&v"(u0), "+&v"(u1), "+&v"(v0), "+&v"(v1), "+&v"(xn)
+        : "v"(x), "v"(F.K[0]), "v"(F.K[1]), "v"(F.K[2]), "v"(F.K[3]), "v"(F.K[4]), "v"(F.K[5]), "v"(F.K[6]),
+          "v"(F.K[7]), "v"(F.K[8]), "v"(F.K[9]), "v"(F.f0), "v"(F.f2), "v"(F.f3), "v"(F.f4));
+    u0 = u0 + v0;
+    u1 = u1 + v1;
+    x = fma(L.bu0, u0, fma(L.bu1, u1, xn));
+    mst1(L.m5, S.dX + 5 * (t + 1) + L.i, x);
+    mst2(L.m0, S.dud + 2 * t, u0, u1);
+}
+
+// NT > 0: the horizon is a compile-time constant and both passes are fully unrolled.
+template <int NT>
+__device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
+    const int N = NT > 0 ? NT : Nrt;
+    const DLane L = dlane(gl, dt);
+    double p = S.QH[QHS * N + L.i];
+#ifdef MPC_SOLVE_LOOP
+    if constexpr (false) {
+#else
+    if constexpr (NT > 0) {
+#endif
+        BwdRec buf[2];
+        load_bwd(S, L, NT - 1, buf[0]);
+#pragma unroll
+        for (int t = NT - 1; t >= 0; --t) {
             sched_fence();
-            fwd_step(S, t, dt, buf[t & 1], x, ln);
+            load_bwd(S, L, t >= 1 ? t - 1 : 0, buf[(NT - t) & 1]);
+            sched_fence();
+            bwd_step(S, L, t, dt, buf[(NT - 1 - t) & 1], p);
         }
     } else {
-        FwdBuf A, B;
-        load_fwd(S, 0, A);
+        BwdRec A, B;
+        load_bwd(S, L, N - 1, A);
+        int t = N - 1;
+        while (true) {
+            sched_fence();
+            load_bwd(S, L, t >= 1 ? t - 1 : 0, B);
+            sched_fence();
+            bwd_step(S, L, t, dt, A, p);
+            if (--t < 0) break;
+            sched_fence();
+            load_bwd(S, L, t >= 1 ? t - 1 : 0, A);
+            sched_fence();
+            bwd_step(S, L, t, dt, B, p);
+            if (--t < 0) break;
+        }
+    }
+#ifdef MPC_SOLVE_SYNC
+    wave_sync();
+#endif
+    double x = 0.0;
+    mst1(L.m5, S.dX + L.i, 0.0);
+#ifdef MPC_SOLVE_LOOP
+    if constexpr (false) {
+#else
+    if constexpr (NT > 0) {
+#endif
+        FwdRec buf[2];
+        load_fwd(S, L, 0, buf[0]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            sched_fence();
+            load_fwd(S, L, t + 1 < NT ? t + 1 : t, buf[(t + 1) & 1]);
+            sched_fence();
+            fwd_step(S, L, t, buf[t & 1], x);
+        }
+    } else {
+        FwdRec A, B;
+        load_fwd(S, L, 0, A);
         int t = 0;
         while (true) {
-            solve_fence();
-            load_fwd(S, t + 1 < N ? t + 1 : t, B);
             sched_fence();
-            fwd_step(S, t, dt, A, x, ln);
+            load_fwd(S, L, t + 1 < N ? t + 1 : t, B);
+            sched_fence();
+            fwd_step(S, L, t, A, x);
             if (++t >= N) break;
-            solve_fence();
-            load_fwd(S, t + 1 < N ? t + 1 : t, A);
             sched_fence();
-            fwd_step(S, t, dt, B, x, ln);
+            load_fwd(S, L, t + 1 < N ? t + 1 : t, A);
+            sched_fence();
+            fwd_step(S, L, t, B, x);
             if (++t >= N) break;
         }
     }
@@ -649,12 +738,12 @@ __device__ void dual_norms(const Lds& S, int N, double dt, double& rdmax, double
     for (int k = N; k >= 1; --k) {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-            mc[st4(a)] += S.yc[4 * k + a];
-            ma[st4(a)] += S.ya[4 * k + a];
+            mc[st4(a)] += S.QR[QRS * k + DQ_YC + a];
+            ma[st4(a)] += S.QR[QRS * k + DQ_YA + a];
         }
         const int t = k - 1;
-        double gc0 = fma(dt, mc[3], S.zc[2 * t]), gc1 = fma(dt, mc[4], S.zc[2 * t + 1]);
-        double ga0 = fma(dt, ma[3], S.za[2 * t]), ga1 = fma(dt, ma[4], S.za[2 * t + 1]);
+        double gc0 = fma(dt, mc[3], S.QR[QRS * t + DQ_ZC]), gc1 = fma(dt, mc[4], S.QR[QRS * t + DQ_ZC + 1]);
+        double ga0 = fma(dt, ma[3], S.QR[QRS * t + DQ_ZA]), ga1 = fma(dt, ma[4], S.QR[QRS * t + DQ_ZA + 1]);
         rdmax = fmax(rdmax, fmax(fabs(gc0 + ga0), fabs(gc1 + ga1)));
         sd = fmax(sd, fmax(fmax(fabs(gc0), fabs(gc1)), fmax(fabs(ga0), fabs(ga1))));
         double y[5];
@@ -842,6 +931,15 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             S.A5[A5S * gl + 2] = dt * (-x[4] * dk);
             S.A5[A5S * gl + 3] = dt * x[4];
             S.A5[A5S * gl + 4] = dt * (x[3] - refk[3]);
+            S.A5[A5S * gl + 5] = dt;      // a04, read by the per-lane gathers (DLane)
+            S.A5[A5S * gl + 6] = 0.0;     // the gathers' zero slot
+            S.A5[A5S * gl + 7] = 0.0;
+        }
+        if (gl <= N) {
+            // the k row of QR is structurally zero (no cost or row touches k); the k entry of QH is
+            // written as zero by every QH writer (QH shares its space with Xr, which is live here)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) S.QR[QRS * gl + 12 + j] = 0.0;
         }
         // cost data of stage k (lookups done by lane k of the group)
         {
@@ -963,17 +1061,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 rxmax = fmax(rxmax, fabs(rx));
                 comp = fma(rs[j], rl[j], fma(rxi[j], rnu[j], comp));
             }
-            double za0 = 0.0, za1 = 0.0;
-            if (live) {
-#pragma unroll
-                for (int j = 0; j < NBOX; ++j) {
-                    const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
-                    rpmax = fmax(rpmax, fabs(rp));
-                    comp = fma(sb[j], lb[j], comp);
-                }
-                za0 = lb[1] - lb[0];
-                za1 = lb[3] - lb[2];
-                double Qs[10], qs[4], yc[4];
+            // dual-residual stage terms of stage k / control k-1: yc (cost), zc (control cost), za (box
+            // multipliers); ya (row multipliers) accumulated above
+            auto dual_terms = [&](double yc[4], double zc[2], double za[2]) {
+                double Qs[10], qs[4];
                 stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
@@ -982,12 +1073,24 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     for (int c = 0; c < 4; ++c) acc = fma(Qs[p4(a, c)], x4[c], acc);
                     yc[a] = acc;
                 }
+                zc[0] = fma(R0, du0, R0 * S.ub[2 * (k - 1)]);
+                zc[1] = fma(R1, du1, R1 * S.ub[2 * (k - 1) + 1]);
+                za[0] = lb[1] - lb[0];
+                za[1] = lb[3] - lb[2];
+            };
+            if (live) {
 #pragma unroll
-                for (int a = 0; a < 4; ++a) { S.yc[4 * k + a] = yc[a]; S.ya[4 * k + a] = ya[a]; }
-                S.zc[2 * (k - 1)] = fma(R0, du0, R0 * S.ub[2 * (k - 1)]);
-                S.zc[2 * (k - 1) + 1] = fma(R1, du1, R1 * S.ub[2 * (k - 1) + 1]);
-                S.za[2 * (k - 1)] = za0;
-                S.za[2 * (k - 1) + 1] = za1;
+                for (int j = 0; j < NBOX; ++j) {
+                    const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
+                    rpmax = fmax(rpmax, fabs(rp));
+                    comp = fma(sb[j], lb[j], comp);
+                }
+                double yc[4], zc[2], za[2];
+                dual_terms(yc, zc, za);
+#pragma unroll
+                for (int a = 0; a < 4; ++a) S.ys[4 * k + a] = yc[a] + ya[a];
+                S.zs[2 * (k - 1)] = zc[0] + za[0];
+                S.zs[2 * (k - 1) + 1] = zc[1] + za[1];
             }
             rpmax = Q.max(rpmax);
             rxmax = Q.max(rxmax);
@@ -1000,6 +1103,20 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 // converged: the polish then makes the active set exact;
                 // the dual residual carries O(eps/mu) multiplier noise, required to 1e4*tol.  Its
                 // adjoint recursion is only run here, once per solve.
+                if (live) {
+                    double yc[4], zc[2], za[2];
+                    dual_terms(yc, zc, za);
+#pragma unroll
+                    for (int a = 0; a < 4; ++a) {
+                        S.QR[QRS * k + DQ_YC + a] = yc[a];
+                        S.QR[QRS * k + DQ_YA + a] = ya[a];
+                    }
+                    S.QR[QRS * (k - 1) + DQ_ZC] = zc[0];
+                    S.QR[QRS * (k - 1) + DQ_ZC + 1] = zc[1];
+                    S.QR[QRS * (k - 1) + DQ_ZA] = za[0];
+                    S.QR[QRS * (k - 1) + DQ_ZA + 1] = za[1];
+                }
+                wave_sync();
                 double rdmax, sd;
                 dual_norms(S, N, dt, rdmax, sd);
                 PROF(3)
@@ -1032,14 +1149,16 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     double Qs[10], qs[4];
                     stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
-                    for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a] + Qs[a];
+                    for (int a = 0; a < 4; ++a)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) S.QR[QRS * k + 4 * st4(a) + c] = Qp[p4(a, c)] + Qs[p4(a, c)];
                     S.Rt[2 * (k - 1)] = R0 + (wb[0] + wb[1]);
                     S.Rt[2 * (k - 1) + 1] = R1 + (wb[2] + wb[3]);
                 }
             }
             wave_sync();
             PROF(4)
-            riccati_factor(S, N, dt, gl);
+            riccati_factor<NT>(S, N, dt, gl);
             PROF(5)
             // -- predictor, corrector (and, if needed, centred) solves ---------------------------------
             double p4v[NR], p5v[NR], pbv[NBOX];
@@ -1106,9 +1225,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     }
                     if (live) {
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) S.qh[4 * k + a] = q4[a] - (S.yc[4 * k + a] + S.ya[4 * k + a]);
-                        S.gh[2 * (k - 1)] = g0 - (S.zc[2 * (k - 1)] + S.za[2 * (k - 1)]);
-                        S.gh[2 * (k - 1) + 1] = g1 - (S.zc[2 * (k - 1) + 1] + S.za[2 * (k - 1) + 1]);
+                        for (int a = 0; a < 4; ++a) S.QH[QHS * k + st4(a)] = q4[a] - S.ys[4 * k + a];
+                        S.QH[QHS * k + 3] = 0.0;
+                        S.QH[QHS * k + 5] = 0.0;
+                        S.gh[2 * (k - 1)] = g0 - S.zs[2 * (k - 1)];
+                        S.gh[2 * (k - 1) + 1] = g1 - S.zs[2 * (k - 1) + 1];
                     }
                 }
                 wave_sync();
@@ -1270,12 +1391,14 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     double Qs[10], qs[4];
                     stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
-                    for (int a = 0; a < 10; ++a) S.Qt[10 * k + a] = Qp[a] + Qs[a];
+                    for (int a = 0; a < 4; ++a)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) S.QR[QRS * k + 4 * st4(a) + c] = Qp[p4(a, c)] + Qs[p4(a, c)];
                     S.Rt[2 * (k - 1)] = R0 + (clb[0] + clb[1]) * (1.0 / POLISH_DELTA);
                     S.Rt[2 * (k - 1) + 1] = R1 + (clb[2] + clb[3]) * (1.0 / POLISH_DELTA);
                 }
                 wave_sync();
-                riccati_factor(S, N, dt, gl);
+                riccati_factor<NT>(S, N, dt, gl);
                 double xp[4] = {x4[0], x4[1], x4[2], x4[3]};
                 pu0 = du0;
                 pu1 = du1;
@@ -1308,8 +1431,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                             double acc = qs[a];
 #pragma unroll
                             for (int c = 0; c < 4; ++c) acc = fma(Qs[p4(a, c)], xp[c], acc);
-                            S.qh[4 * k + a] = q4[a] - acc;
+                            S.QH[QHS * k + st4(a)] = q4[a] - acc;
                         }
+                        S.QH[QHS * k + 3] = 0.0;
+                        S.QH[QHS * k + 5] = 0.0;
                         S.gh[2 * (k - 1)] = g0 - fma(R0, pu0, R0 * S.ub[2 * (k - 1)]);
                         S.gh[2 * (k - 1) + 1] = g1 - fma(R1, pu1, R1 * S.ub[2 * (k - 1) + 1]);
                     }
@@ -1841,7 +1966,7 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     // horizon-specialised kernels for the BASELINE horizons that pay for their code size (N = 20)
 #define MPC_LAUNCH_GL(MODEV)                                                                   \
     do {                                                                                       \
-        if (kp.N == 20) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 20); else MPC_LAUNCH(32, false, MODEV, 20); } \
+        if (kp.N == 20 && !MPC_NO_NT20) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 20); else MPC_LAUNCH(32, false, MODEV, 20); } \
         else if (GL == 16) { if (with_obs) MPC_LAUNCH(16, true, MODEV, 0); else MPC_LAUNCH(16, false, MODEV, 0); } \
         else if (GL == 32) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 0); else MPC_LAUNCH(32, false, MODEV, 0); } \
         else { if (with_obs) MPC_LAUNCH(64, true, MODEV, 0); else MPC_LAUNCH(64, false, MODEV, 0); } \
