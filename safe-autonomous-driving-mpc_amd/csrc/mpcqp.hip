@@ -233,7 +233,9 @@ __device__ __forceinline__ double frsqrt(double x) {
     double y = __builtin_amdgcn_rsq(x);
     const double h = 0.5 * x;
     y = y * fma(-h * y, y, 1.5);
+#ifndef MPC_RSQ1
     y = y * fma(-h * y, y, 1.5);
+#endif
     return y;
 }
 // 1/x to full double precision: v_rcp_f64 + two Newton steps (no IEEE division sequence)
@@ -839,6 +841,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                  int* __restrict__ itersg, int* __restrict__ wlist, int* __restrict__ wcount) {
     constexpr int G = WAVE / GL;
     constexpr int NR = OBS ? NROW : NROW - 2;    // soft rows held per lane (6, 7: obstacle rows)
+    // the Riccati solves are fully unrolled (compile-time horizon) in the obstacle-free kernels only:
+    // the obstacle kernels hold 9 rows per lane, and there the looped solves need fewer registers
+    // (fewer spills; measured C3 1.34 -> 1.24 ms)
+    constexpr int NTR = OBS ? 0 : NT;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int ln = threadIdx.x;
     const int grp = ln / GL, gl = ln % GL;
@@ -1234,7 +1240,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 }
                 wave_sync();
                 PROF(6)
-                riccati_solve<NT>(S, N, dt, gl);
+                riccati_solve<NTR>(S, N, dt, gl);
                 PROF(7)
                 // row directions and the largest feasible step
                 double dx4[4];
@@ -1439,7 +1445,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         S.gh[2 * (k - 1) + 1] = g1 - fma(R1, pu1, R1 * S.ub[2 * (k - 1) + 1]);
                     }
                     wave_sync();
-                    riccati_solve<NT>(S, N, dt, gl);
+                    riccati_solve<NTR>(S, N, dt, gl);
                     {
                         double dx4[4];
 #pragma unroll
