@@ -227,6 +227,23 @@ __device__ __forceinline__ double bsign(int j) { return (j & 1) ? -1.0 : 1.0; } 
 __device__ __forceinline__ double dot4(const double c[4], const double x[4]) {
     return fma(c[0], x[0], fma(c[1], x[1], fma(c[2], x[2], c[3] * x[3])));
 }
+// structural nonzeros of the soft-row coefficient vectors (row_coef): (s,d,o,v) entry a of row j
+__host__ __device__ constexpr bool row_nz(int j, int a) {
+    return j <= 1 ? a == 1 : (j <= 5 ? (a == 1 || a == 2) : (j == 6 ? a == 0 : (j == 7 ? (a == 0 || a == 3) : a == 3)));
+}
+// dot4 over the structural nonzeros only, in dot4's association order (identical for finite x: the
+// skipped terms are exact zeros); the multiplications by literal zeros are not folded by the compiler
+__device__ __forceinline__ double rdot(int j, const double c[4], const double x[4]) {
+    double acc = 0.0;
+    bool first = true;
+#pragma unroll
+    for (int a = 3; a >= 0; --a)
+        if (row_nz(j, a)) {
+            acc = first ? c[a] * x[a] : fma(c[a], x[a], acc);
+            first = false;
+        }
+    return acc;
+}
 // 1/sqrt(x) to full double precision: v_rsq_f64 + two Newton steps (the Cholesky pivots only
 // enter as reciprocals; the IEEE sqrt sequence costs ~100 cycles of dependent latency on gfx950)
 __device__ __forceinline__ double frsqrt(double x) {
@@ -438,6 +455,9 @@ struct DLane {
     unsigned long long m5, m0; // lanes i < 5 of every group / lane 0 of every group
 };
 __device__ __forceinline__ DLane dlane(int gl, double dt) {
+    // opaque lane index: the constants are rebuilt at every recursion (a few VALU) instead of being
+    // hoisted out of the interior-point loop and held in registers across the row phases
+    asm volatile("" : "+v"(gl));
     DLane D;
     D.i = gl < 5 ? gl : 4;
     const int z = 6;
@@ -883,11 +903,15 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 
     const int k = gl + 1;            // stage of this lane
     const bool live = k <= N;        // lane owns the rows of stage k and the boxes of control k-1
-    bool ron[NR];
+    // rowon: the row exists for this instance (group-uniform: the obstacle rows need obstacles);
+    // ron = rowon on a live lane.  The per-iteration phases use rowon only: dead lanes (stages past N)
+    // compute discarded values and are masked where lane values meet (the group reductions)
+    bool ron[NR], rowon[NR];
     double cf[NR][4];
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
-        ron[j] = live && ((rid<OBS>(j) != 6 && rid<OBS>(j) != 7) || has_obs);
+        rowon[j] = (rid<OBS>(j) != 6 && rid<OBS>(j) != 7) || has_obs;
+        ron[j] = live && rowon[j];
         row_coef(rid<OBS>(j), hL, Pr.L, Pr.tgap, cf[j]);
     }
 
@@ -1058,8 +1082,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             double ya[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int j = 0; j < NR; ++j) {
-                if (!ron[j]) continue;
-                const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
+                if (!rowon[j]) continue;
+                const double rp = rdot(rid<OBS>(j), cf[j], x4) + rxi[j] - rs[j] - bk[j];
                 const double rx = rho - rl[j] - rnu[j];
 #pragma unroll
                 for (int a = 0; a < 4; ++a) ya[a] = fma(-rl[j], cf[j][a], ya[a]);
@@ -1098,9 +1122,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 S.zs[2 * (k - 1)] = zc[0] + za[0];
                 S.zs[2 * (k - 1) + 1] = zc[1] + za[1];
             }
-            rpmax = Q.max(rpmax);
-            rxmax = Q.max(rxmax);
-            comp = Q.sum(comp);
+            rpmax = Q.max(live ? rpmax : 0.0);
+            rxmax = Q.max(live ? rxmax : 0.0);
+            comp = Q.sum(live ? comp : 0.0);
             wave_sync();
             PROF(2)
             mu = comp / Mtot;
@@ -1138,7 +1162,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 for (int j = 0; j < NR; ++j) {
                     il[j] = frcp(rl[j]);
                     inu[j] = frcp(rnu[j]);
-                    wv[j] = ron[j] ? frcp(fma(rs[j], il[j], rxi[j] * inu[j])) : 0.0;   // 1/d
+                    wv[j] = rowon[j] ? frcp(fma(rs[j], il[j], rxi[j] * inu[j])) : 0.0;   // 1/d
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -1185,10 +1209,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 auto row_wr = [&](int j) {
                     const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
                     const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
-                    const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
+                    const double rp = rdot(rid<OBS>(j), cf[j], x4) + rxi[j] - rs[j] - bk[j];
                     const double rx = rho - rl[j] - rnu[j];
                     const double rh = -rp - r4 * il[j] + fma(rxi[j], rx, r5) * inu[j];
-                    return ron[j] ? rh * wv[j] : 0.0;
+                    return rowon[j] ? rh * wv[j] : 0.0;
                 };
                 auto box_wr = [&](int j) {
                     const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
@@ -1206,10 +1230,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         } else {
                             const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
                             const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
-                            const double rp = dot4(cf[j], x4) + rxi[j] - rs[j] - bk[j];
+                            const double rp = rdot(rid<OBS>(j), cf[j], x4) + rxi[j] - rs[j] - bk[j];
                             const double rx = rho - rl[j] - rnu[j];
                             const double rh = -rp - r4 * il[j] + fma(rxi[j], rx, r5) * inu[j];
-                            wr[j] = ron[j] ? rh * wv[j] : 0.0;
+                            wr[j] = rowon[j] ? rh * wv[j] : 0.0;
                             w = wr[j];
                         }
 #pragma unroll
@@ -1256,11 +1280,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double rx = rho - rl[j] - rnu[j];
                     double wj;
                     if constexpr (OBS) wj = row_wr(j); else wj = wr[j];
-                    const double dl = fma(-wv[j], dot4(cf[j], dx4), wj);
+                    const double dl = fma(-wv[j], rdot(rid<OBS>(j), cf[j], dx4), wj);
                     const double ds = -fma(rs[j], dl, r4) * il[j];
                     const double dn = rx - dl;
                     const double dxi = -fma(rxi[j], dn, r5) * inu[j];
-                    const bool on = ron[j];
+                    const bool on = rowon[j];
                     dsv[j] = on ? ds : 0.0;
                     dlv[j] = on ? dl : 0.0;
                     dxv[j] = on ? dxi : 0.0;
@@ -1278,26 +1302,24 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     if constexpr (OBS) wj = box_wr(j); else wj = wrb[j];
                     const double dl = fma(-wb[j] * bsign(j), (j < 2 ? dd0 : dd1), wj);
                     const double ds = -fma(sb[j], dl, r4) * ilb[j];
-                    dsb[j] = live ? ds : 0.0;
-                    dlb[j] = live ? dl : 0.0;
+                    dsb[j] = ds;
+                    dlb[j] = dl;
                     if (dsb[j] < 0.0) amax = fmin(amax, -sb[j] * __builtin_amdgcn_rcp(dsb[j]));
                     if (dlb[j] < 0.0) amax = fmin(amax, -lb[j] * __builtin_amdgcn_rcp(dlb[j]));
                 }
-                amax = Q.min(amax);
+                amax = Q.min(live ? amax : 1.0);
                 // complementarity after the step (pass 0: at the full affine step length)
                 const double a_try = (pass == 0) ? amax : fmin(1.0, TAU * amax);
                 double ca = 0.0;
 #pragma unroll
                 for (int j = 0; j < NR; ++j)
-                    if (ron[j])
+                    if (rowon[j])
                         ca += fma(a_try, dsv[j], rs[j]) * fma(a_try, dlv[j], rl[j]) +
                               fma(a_try, dxv[j], rxi[j]) * fma(a_try, dnv[j], rnu[j]);
-                if (live) {
 #pragma unroll
-                    for (int j = 0; j < NBOX; ++j) ca += fma(a_try, dsb[j], sb[j]) * fma(a_try, dlb[j], lb[j]);
-                    if (!(fabs(dd0) < INFINITY && fabs(dd1) < INFINITY)) ca = NAN;   // breakdown guard input
-                }
-                ca = Q.sum(ca);
+                for (int j = 0; j < NBOX; ++j) ca += fma(a_try, dsb[j], sb[j]) * fma(a_try, dlb[j], lb[j]);
+                if (!(fabs(dd0) < INFINITY && fabs(dd1) < INFINITY)) ca = NAN;   // breakdown guard input
+                ca = Q.sum(live ? ca : 0.0);
                 PROF(11)
                 if (pass == 0) {
                     const double r = ca / comp;
@@ -1543,6 +1565,14 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------
     PROF(9)
+    // x0 is re-read here (an opaque index defeats CSE with the first load) rather than held in
+    // registers across the interior point, where it would be spilled to scratch
+    {
+        int bo = b;
+        asm volatile("" : "+v"(bo));
+#pragma unroll
+        for (int j = 0; j < 5; ++j) x0[j] = x0g[5 * (size_t)bo + j];
+    }
     predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
     if (MODE == MODE_XO && !xo_ok) {
         // not certified: defer to the MODE_IPM launch (group-uniform)
