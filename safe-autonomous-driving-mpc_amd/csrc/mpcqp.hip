@@ -250,9 +250,7 @@ __device__ __forceinline__ double frsqrt(double x) {
     double y = __builtin_amdgcn_rsq(x);
     const double h = 0.5 * x;
     y = y * fma(-h * y, y, 1.5);
-#ifndef MPC_RSQ1
     y = y * fma(-h * y, y, 1.5);
-#endif
     return y;
 }
 // 1/x to full double precision: v_rcp_f64 + two Newton steps (no IEEE division sequence)
@@ -1167,7 +1165,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
                         for (int c = a; c < 4; ++c)
-                            if (cf[j][a] != 0.0 && cf[j][c] != 0.0)
+                            if (row_nz(rid<OBS>(j), a) && row_nz(rid<OBS>(j), c))
                                 Qp[p4(a, c)] = fma(wv[j] * cf[j][a], cf[j][c], Qp[p4(a, c)]);
                 }
 #pragma unroll
@@ -1238,7 +1236,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         }
 #pragma unroll
                         for (int a = 0; a < 4; ++a)
-                            if (cf[j][a] != 0.0) q4[a] = fma(cf[j][a], w, q4[a]);
+                            if (row_nz(rid<OBS>(j), a)) q4[a] = fma(cf[j][a], w, q4[a]);
                     }
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) {
@@ -1413,7 +1411,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         for (int a = 0; a < 4; ++a)
 #pragma unroll
                             for (int c = a; c < 4; ++c)
-                                if (cf[j][a] != 0.0 && cf[j][c] != 0.0)
+                                if (row_nz(rid<OBS>(j), a) && row_nz(rid<OBS>(j), c))
                                     Qp[p4(a, c)] = fma(w * cf[j][a], cf[j][c], Qp[p4(a, c)]);
                     }
                     double Qs[10], qs[4];
@@ -1435,7 +1433,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     // exact KKT residual of the equality QP -> LQR right-hand side
                     double r2[NR], r2b[NBOX];
 #pragma unroll
-                    for (int j = 0; j < NR; ++j) r2[j] = (cls[j] == 1) ? bkp[j] - dot4(cf[j], xp) : 0.0;
+                    for (int j = 0; j < NR; ++j) r2[j] = (cls[j] == 1) ? bkp[j] - rdot(rid<OBS>(j), cf[j], xp) : 0.0;
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) r2b[j] = (clb[j] == 1) ? bbp[j] - bsign(j) * (j < 2 ? pu0 : pu1) : 0.0;
                     if (live) {
@@ -1445,7 +1443,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                             const double wgt = (cls[j] == 2) ? rho : (cls[j] == 1 ? tl[j] + r2[j] * (1.0 / POLISH_DELTA) : 0.0);
 #pragma unroll
                             for (int a = 0; a < 4; ++a)
-                                if (cf[j][a] != 0.0) q4[a] = fma(cf[j][a], wgt, q4[a]);
+                                if (row_nz(rid<OBS>(j), a)) q4[a] = fma(cf[j][a], wgt, q4[a]);
                         }
 #pragma unroll
                         for (int j = 0; j < NBOX; ++j) {
@@ -1474,7 +1472,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
 #pragma unroll
                         for (int j = 0; j < NR; ++j)
-                            if (cls[j] == 1) tl[j] += (r2[j] - dot4(cf[j], dx4)) * (1.0 / POLISH_DELTA);
+                            if (cls[j] == 1) tl[j] += (r2[j] - rdot(rid<OBS>(j), cf[j], dx4)) * (1.0 / POLISH_DELTA);
                         const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
 #pragma unroll
                         for (int j = 0; j < NBOX; ++j)
@@ -1505,7 +1503,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     flip[j] = false;
                     if (!ron[j]) continue;
                     const double bsc = 1.0 + fabs(bkp[j]);
-                    const double r = dot4(cf[j], xp) - bkp[j];
+                    const double r = rdot(rid<OBS>(j), cf[j], xp) - bkp[j];
                     bool badv;
                     if (cls[j] == 1) {
                         badv = tl[j] < -1e-9 * lmax || tl[j] > rho * (1.0 + 1e-9) || fabs(r) > 1e-7 * bsc;
