@@ -29,6 +29,9 @@
 #define WAVE 64
 #ifndef MPC_NO_NT20
 #define MPC_NO_NT20 0
+#ifndef MPC_EXEC5
+#define MPC_EXEC5 1     // recursions under exec = lanes 0..4 of each group (0: per-store masks)
+#endif
 #endif
 #define NROW 9
 #define NBOX 4
@@ -418,7 +421,16 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // s_and_saveexec writes SCC, hence the "scc" clobber (a loop condition held in SCC across the store
 // would otherwise be lost).
 __device__ __forceinline__ unsigned lds_off(const double* p) { return (unsigned)(size_t)p; }
-#ifdef MPC_NO_MST
+#if MPC_EXEC5
+// the recursions run with exec narrowed to lanes 0..4 of each group (rec_lanes below), so every store
+// is a plain store: the values of lane-0 records (Si, kk, dud) are group-uniform, and all five lanes
+// write the same value to the same address
+__device__ __forceinline__ void mst1(unsigned long long, const double* p, double v) { *const_cast<double*>(p) = v; }
+__device__ __forceinline__ void mst2(unsigned long long, const double* p, double v0, double v1) {
+    const_cast<double*>(p)[0] = v0;
+    const_cast<double*>(p)[1] = v1;
+}
+#elif defined(MPC_NO_MST)
 __device__ __forceinline__ void mst1(unsigned long long mask, const double* p, double v) {
     if ((mask >> __lane_id()) & 1ull) *const_cast<double*>(p) = v;
 }
@@ -573,7 +585,7 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
 }
 // NT > 0: horizon fixed at compile time, stages fully unrolled (immediate LDS offsets, no loop control)
 template <int NT>
-__device__ void riccati_factor(const Lds& S, int Nrt, double dt, int gl) {
+__device__ __forceinline__ void riccati_factor_lanes(const Lds& S, int Nrt, double dt, int gl) {
     const int N = NT > 0 ? NT : Nrt;
     const DLane L = dlane(gl, dt);
     const double dt2 = dt * dt;
@@ -612,6 +624,12 @@ __device__ void riccati_factor(const Lds& S, int Nrt, double dt, int gl) {
             if (--t < 0) break;
         }
     }
+}
+// the recursion runs on lanes 0..4 of each group only (exec narrowed): the other lanes would compute
+// discarded values, and with them out of exec every store is a plain store
+template <int NT>
+__device__ void riccati_factor(const Lds& S, int Nrt, double dt, int gl) {
+    if (!MPC_EXEC5 || gl < 5) riccati_factor_lanes<NT>(S, Nrt, dt, gl);
     wave_sync();
 }
 
@@ -676,7 +694,7 @@ __device__ __forceinline__ void fwd_step(const Lds& S, const DLane& L, int t, co
 
 // NT > 0: the horizon is a compile-time constant and both passes are fully unrolled.
 template <int NT>
-__device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
+__device__ __forceinline__ void riccati_solve_lanes(const Lds& S, int Nrt, double dt, int gl) {
     const int N = NT > 0 ? NT : Nrt;
     const DLane L = dlane(gl, dt);
     double p = S.QH[QHS * N + L.i];
@@ -711,9 +729,6 @@ __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
             if (--t < 0) break;
         }
     }
-#ifdef MPC_SOLVE_SYNC
-    wave_sync();
-#endif
     double x = 0.0;
     mst1(L.m5, S.dX + L.i, 0.0);
 #ifdef MPC_SOLVE_LOOP
@@ -747,6 +762,10 @@ __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
             if (++t >= N) break;
         }
     }
+}
+template <int NT>
+__device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
+    if (!MPC_EXEC5 || gl < 5) riccati_solve_lanes<NT>(S, Nrt, dt, gl);
     wave_sync();
 }
 

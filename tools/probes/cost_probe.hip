@@ -217,6 +217,51 @@ __global__ void k(double* out, long long* cyc, double a, double b) {
         cyc[14] = t1 - t0;
         acc += d0;
     }
+    // 15. recursion pattern: each link's DPP source is the previous link's result (ping-pong a <-> b)
+    {
+        double a0 = x, b0 = x * 0.5, c = b;
+        t0 = __builtin_amdgcn_s_memtime();
+        for (int r = 0; r < REP; ++r) {
+            asm volatile("s_nop 1\n\t"
+                "v_fmac_f64_dpp %0, %1, %2 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\ts_nop 1\n\t"
+                "v_fmac_f64_dpp %1, %0, %2 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\ts_nop 1\n\t"
+                "v_fmac_f64_dpp %0, %1, %2 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\ts_nop 1\n\t"
+                "v_fmac_f64_dpp %1, %0, %2 row_newbcast:4 row_mask:0xf bank_mask:0xf"
+                : "+v"(a0), "+v"(b0) : "v"(c));
+        }
+        t1 = __builtin_amdgcn_s_memtime();
+        cyc[15] = t1 - t0;
+        acc += a0 + b0;
+    }
+    // 16. dependent v_add_f64 chain
+    {
+        double z = x;
+        t0 = __builtin_amdgcn_s_memtime();
+        for (int r = 0; r < REP * 4; ++r) { z = z + b; asm volatile("" : "+v"(z)); }
+        t1 = __builtin_amdgcn_s_memtime();
+        cyc[16] = t1 - t0;
+        acc += z;
+    }
+    // 17. dependent v_fmac_f64 chain through the multiplicand (x <- c + x * d), plain VALU
+    {
+        double z = x, c = a, d = b;
+        t0 = __builtin_amdgcn_s_memtime();
+        for (int r = 0; r < REP; ++r) {
+            asm volatile("v_fma_f64 %0, %0, %2, %1\n\tv_fma_f64 %0, %0, %2, %1\n\t"
+                         "v_fma_f64 %0, %0, %2, %1\n\tv_fma_f64 %0, %0, %2, %1"
+                         : "+v"(z) : "v"(c), "v"(d));
+        }
+        t1 = __builtin_amdgcn_s_memtime();
+        cyc[17] = t1 - t0;
+        acc += z;
+    }
+    // 18. s_memtime reference: 4 * REP dependent v_add_f64 vs s_sleep-free empty loop
+    {
+        t0 = __builtin_amdgcn_s_memtime();
+        for (int r = 0; r < REP; ++r) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7");
+        t1 = __builtin_amdgcn_s_memtime();
+        cyc[18] = t1 - t0;
+    }
     out[ln] = acc;
 }
 
@@ -224,14 +269,14 @@ int main() {
     double* o;
     long long* c;
     hipMalloc(&o, 64 * 8);
-    hipMalloc(&c, 16 * 8);
-    hipMemset(c, 0, 16 * 8);
-    long long h[16];
+    hipMalloc(&c, 32 * 8);
+    hipMemset(c, 0, 32 * 8);
+    long long h[32];
     for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, o, c, 1e-3, 0.999);
         hipDeviceSynchronize();
     }
-    hipMemcpy(h, c, 16 * 8, hipMemcpyDeviceToHost);
+    hipMemcpy(h, c, 32 * 8, hipMemcpyDeviceToHost);
     // s_memtime ticks; per unit below
     printf("indep v_fma_f64            %7.2f per instr\n", (double)h[0] / (REP * 4 * 8));
     printf("ds_read_b128 bcast, 64 ln  %7.2f per read (incl. 1 add)\n", (double)h[1] / (REP * 16));
@@ -248,5 +293,9 @@ int main() {
     printf("indep v_fmac_f64_dpp       %7.2f per instr (incl. s_nop 1 per 8)\n", (double)h[12] / (REP * 16));
     printf("indep v_fmac_f64 (asm)     %7.2f per instr (incl. s_nop 1 per 8)\n", (double)h[13] / (REP * 16));
     printf("dependent v_fmac_f64_dpp   %7.2f per link\n", (double)h[14] / (REP * 4));
+    printf("dpp source chain (+nop 1)  %7.2f per link\n", (double)h[15] / (REP * 4));
+    printf("dependent v_add_f64        %7.2f per link\n", (double)h[16] / (REP * 4));
+    printf("dependent v_fma_f64 (asm)  %7.2f per link\n", (double)h[17] / (REP * 4));
+    printf("s_nop 7 (8 cycles?)        %7.2f per nop\n", (double)h[18] / (REP * 4));
     return 0;
 }
