@@ -29,9 +29,6 @@
 #define WAVE 64
 #ifndef MPC_NO_NT20
 #define MPC_NO_NT20 0
-#ifndef MPC_EXEC5
-#define MPC_EXEC5 1     // recursions under exec = lanes 0..4 of each group (0: per-store masks)
-#endif
 #endif
 #define NROW 9
 #define NBOX 4
@@ -140,22 +137,22 @@ __device__ void get_control(const DevTable& t, double s, double* out) {
 // starts 16-B aligned, so each pair is one ds_read_b128 (4 LDS cycles) instead of a ds_read2_b64 (8).
 // The Riccati recursions are lane-distributed (section "distributed recursions" below): lane i = 0..4
 // of a group holds row i of P / component i of the state, so the records they read per lane are laid
-// out by row: QR (row i of the stage Hessian), QH (component i of the linear term), KP (column i of K).
+// out by row: QR (row i of the stage Hessian), QH (component i of the linear term); KR holds K by rows.
 #define A5S 8          // stride of A5: a12, a14, a20, a23, a24, dt, 0, 0 (the zeros and dt serve the
                        // per-lane coefficient gathers of the distributed recursions)
 #define SIS 4          // stride of Si (3 used)
 #define QRS 20         // stride of QR: rows i = 0..4 (s,d,o,k,v) x columns (s,d,o,v); row 3 (k) zero
 #define QHS 6          // stride of QH: (s,d,o,k,v) with k = 0, one pad
+#define KRS 12         // stride of KR: rows r = 0, 1 of K_t, each (K(r,0..4), kk_r)
 struct Lds {
     double* A5;    // [N][A5S]
     double* cst;   // [N+1][6]  cost data of stage k: (-d_ref', -o_ref', -v_ref') and the residuals r_d, r_o, r_v
     double* QR;    // [N+1][QRS] Riccati stage Hessians (barrier / penalty augmented), by row
     double* Rt;    // [N][2]
-    double* KP;    // [N][10]   Riccati gains by column: (K(0,i), K(1,i)), i = 0..4
+    double* KR;    // [N][KRS]  Riccati gains by row, K(r,0..4), with the solve's feed-forward kk_r in slot 5
     double* Si;    // [N][SIS]  (1/l00, l10, 1/l11) of S_t = Ls Ls'
     double* QH;    // [N+1][QHS] LQR stage linear terms (state)
     double* gh;    // [N][2]    LQR stage linear terms (control)
-    double* kk;    // [N][2]
     double* Xr;    // [N+1][5]  nominal rollout (setup, outputs); aliases QH, which is dead then
     double* dX;    // [N+1][5]  rollout of the direction
     double* dud;   // [N][2]    direction dU
@@ -174,7 +171,7 @@ struct Lds {
 
 __host__ __device__ inline int lds_doubles(int N) {
     int NP = N + 1;
-    int n = N * A5S + NP * 6 + NP * QRS + N * 2 + N * 10 + N * SIS + NP * QHS + N * 2 + N * 2 + N * 2 + NP * 4 +
+    int n = N * A5S + NP * 6 + NP * QRS + N * 2 + N * KRS + N * SIS + NP * QHS + N * 2 + N * 2 + NP * 4 +
             N * 2 + N * 2 + NP * 5;
     return (n + 1) & ~1;     // groups stay 16-B aligned
 }
@@ -187,14 +184,13 @@ __device__ inline Lds carve(double* p, int N) {
     L.cst = p; p += NP * 6;
     L.QR = p; p += NP * QRS;
     L.Rt = p; p += N * 2;
-    L.KP = p; p += N * 10;
+    L.KR = p; p += N * KRS;
     L.Si = p; p += N * SIS;
     L.QH = p;
     L.Xr = p;                 // Xr [NP][5] and kap [NP] share QH's NP * 6 doubles
     L.kap = p + NP * 5;
     p += NP * QHS;
     L.gh = p; p += N * 2;
-    L.kk = p; p += N * 2;
     L.dud = p; p += N * 2;
     L.ys = p; p += NP * 4;
     L.zs = p; p += N * 2;
@@ -413,42 +409,6 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // s_nop 1 covers the VALU-write -> DPP-read hazard (2 wait states) of the sources.
 #define DPPF(d, s, c, L) "v_fmac_f64_dpp " d ", " s ", " c " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
 
-// branch-free masked LDS stores: exec is narrowed to `mask` (wave-uniform lane mask) inside one asm
-// statement, so the compiler sees straight-line code (no basic-block split around the store) and can
-// interleave the producing chain with the rest of the step.  The compiler does not count these LDS
-// ops in its lgkmcnt bookkeeping, which only makes its own waits more conservative; every reader of
-// these records runs after them in program order on the same wave (LDS returns in order).
-// s_and_saveexec writes SCC, hence the "scc" clobber (a loop condition held in SCC across the store
-// would otherwise be lost).
-__device__ __forceinline__ unsigned lds_off(const double* p) { return (unsigned)(size_t)p; }
-#if MPC_EXEC5
-// the recursions run with exec narrowed to lanes 0..4 of each group (rec_lanes below), so every store
-// is a plain store: the values of lane-0 records (Si, kk, dud) are group-uniform, and all five lanes
-// write the same value to the same address
-__device__ __forceinline__ void mst1(unsigned long long, const double* p, double v) { *const_cast<double*>(p) = v; }
-__device__ __forceinline__ void mst2(unsigned long long, const double* p, double v0, double v1) {
-    const_cast<double*>(p)[0] = v0;
-    const_cast<double*>(p)[1] = v1;
-}
-#elif defined(MPC_NO_MST)
-__device__ __forceinline__ void mst1(unsigned long long mask, const double* p, double v) {
-    if ((mask >> __lane_id()) & 1ull) *const_cast<double*>(p) = v;
-}
-__device__ __forceinline__ void mst2(unsigned long long mask, const double* p, double v0, double v1) {
-    if ((mask >> __lane_id()) & 1ull) { const_cast<double*>(p)[0] = v0; const_cast<double*>(p)[1] = v1; }
-}
-#else
-__device__ __forceinline__ void mst1(unsigned long long mask, const double* p, double v) {
-    unsigned long long tmp;
-    asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write_b64 %2, %3\n\ts_mov_b64 exec, %0"
-                 : "=&s"(tmp) : "s"(mask), "v"(lds_off(p)), "v"(v) : "memory", "scc");
-}
-__device__ __forceinline__ void mst2(unsigned long long mask, const double* p, double v0, double v1) {
-    unsigned long long tmp;
-    asm volatile("s_and_saveexec_b64 %0, %1\n\tds_write2_b64 %2, %3, %4 offset1:1\n\ts_mov_b64 exec, %0"
-                 : "=&s"(tmp) : "s"(mask), "v"(lds_off(p)), "v"(v0), "v"(v1) : "memory", "scc");
-}
-#endif
 
 // Per-lane constants of the distributed recursions.  A_t = I + J'_t with J' nonzero in rows 0..2 only:
 // J'(0,4) = dt, J'(1,2) = a12, J'(1,4) = a14, J'(2,0) = a20, J'(2,3) = a23, J'(2,4) = a24.  Lane i needs
@@ -459,10 +419,11 @@ struct DLane {
     int i;                     // row / component of this lane (clamped to 4 for lanes >= 5)
     int oe1, oe2, of0, of2, of3, of4;
     double e0;                 // J'(0,i) = dt for i = 4 (constant)
-    double bu0, bu1;           // B(i,:) = dt e3 / dt e4
+    double bu;                 // B(i,:) u = bu * u_r: dt on lanes 3 (r = 0) and 4 (r = 1), else 0
+    int kr, ur;                // K row r the lane reads in the forward solve (offset kr = 6 r in KR), r
+    int ps;                    // slot of p_i in the backward solve's co-state record: (i + 2) % 5
     double k0, k1, k2, k3;     // symmetrisation: lane keeps its own P(i,j) when i <= j
     double r1, r2, r3, r4;     // lane is row 1, 2, 3, 4
-    unsigned long long m5, m0; // lanes i < 5 of every group / lane 0 of every group
 };
 __device__ __forceinline__ DLane dlane(int gl, double dt) {
     // opaque lane index: the constants are rebuilt at every recursion (a few VALU) instead of being
@@ -478,8 +439,10 @@ __device__ __forceinline__ DLane dlane(int gl, double dt) {
     D.of3 = gl == 2 ? 3 : z;
     D.of4 = gl == 0 ? 5 : (gl == 1 ? 1 : (gl == 2 ? 4 : z));
     D.e0 = gl == 4 ? dt : 0.0;
-    D.bu0 = gl == 3 ? dt : 0.0;
-    D.bu1 = gl == 4 ? dt : 0.0;
+    D.bu = gl >= 3 ? dt : 0.0;
+    D.ur = gl >= 4 ? 1 : 0;
+    D.kr = 6 * D.ur;
+    D.ps = gl >= 3 ? gl - 3 : gl + 2;
     D.k0 = gl <= 0 ? 1.0 : 0.0;
     D.k1 = gl <= 1 ? 1.0 : 0.0;
     D.k2 = gl <= 2 ? 1.0 : 0.0;
@@ -488,8 +451,6 @@ __device__ __forceinline__ DLane dlane(int gl, double dt) {
     D.r2 = gl == 2 ? 1.0 : 0.0;
     D.r3 = gl == 3 ? 1.0 : 0.0;
     D.r4 = gl == 4 ? 1.0 : 0.0;
-    D.m5 = __ballot(gl < 5);
-    D.m0 = __ballot(gl == 0);
     return D;
 }
 
@@ -551,9 +512,13 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
     const double w1 = fma(c1, v4, c2 * w0);
     const double K1 = -w1 * il11;
     const double K0 = -(w0 + l10 * K1) * il00;
-    mst2(L.m5, S.KP + 10 * t + 2 * L.i, K0, K1);
-    mst2(L.m0, S.Si + SIS * t, il00, l10);
-    mst1(L.m0, S.Si + SIS * t + 2, il11);
+    // K by rows (lane i writes column i); the Cholesky factor of S is group-uniform: all five lanes write
+    // the same values
+    S.KR[KRS * t + L.i] = K0;
+    S.KR[KRS * t + 6 + L.i] = K1;
+    S.Si[SIS * t] = il00;
+    S.Si[SIS * t + 1] = l10;
+    S.Si[SIS * t + 2] = il11;
     if (upd) {
         // P(i,j) = A'M(i,j) - W1_i W1_j - W0_i W0_j + Qt(i,j)
         const double nw0 = -w0, nw1 = -w1;
@@ -629,73 +594,83 @@ __device__ __forceinline__ void riccati_factor_lanes(const Lds& S, int Nrt, doub
 // discarded values, and with them out of exec every store is a plain store
 template <int NT>
 __device__ void riccati_factor(const Lds& S, int Nrt, double dt, int gl) {
-    if (!MPC_EXEC5 || gl < 5) riccati_factor_lanes<NT>(S, Nrt, dt, gl);
+    if (gl < 5) riccati_factor_lanes<NT>(S, Nrt, dt, gl);
     wave_sync();
 }
 
 // LQR solve with the factorisation: linear terms -QH (stages 1..N), -gh (controls).  Writes dud
-// (controls) and dX (states, x_0 = 0).  Backward: p_t = A_t'p + QH_t + K_t'h, h = gh_t + B'p,
-// kk_t = S_t^-1 h (lane i holds p_i); forward: u_t = kk_t + K_t x, x <- A_t x + B u (lane i holds x_i).
-// Restates riccati_solve() of oracle/mpc_oracle.c.
-struct BwdRec { double g0, g1, si0, si1, si2, e1, e2, K0, K1, qi; };
-struct FwdRec { double kk0, kk1, K[10], f0, f2, f3, f4; };
+// (controls) and dX (states, x_0 = 0).  Three phases (restates riccati_solve() of oracle/mpc_oracle.c):
+//  1. backward, lanes 0..4 (lane i holds p_i): p_t = (A_t + B K_t)' p_{t+1} + QH_t + K_t' gh_t, the
+//     closed-loop form (one accumulator chain of five broadcast FMAs per stage);
+//  2. stage-parallel, lane t: kk_t = S_t^-1 (gh_t + B' p_{t+1}) into slot 5 of the K rows;
+//  3. forward, lanes 0..4 (lane i holds x_i): u_r = kk_r + K_t(r,:) x, x <- A_t x + B u.
+// The co-states p_{t+1} pass from phase 1 to phase 2 through QR (dead between factorisations), in
+// record slots (p3, p4, p0, p1, p2) so that phase 2 reads (p3, p4) with one ds_read_b128.
+struct BwdRec { double g0, g1, qi, K0, K1, e1, e2; };
+struct FwdRec { double K[5], kk, f0, f2, f3, f4; };
 __device__ __forceinline__ void load_bwd(const Lds& S, const DLane& L, int t, BwdRec& B) {
-    double pad;
     const double* a5 = S.A5 + A5S * t;
     ld2(S.gh + 2 * t, B.g0, B.g1);
-    ld2(S.Si + SIS * t, B.si0, B.si1);
-    ld2(S.Si + SIS * t + 2, B.si2, pad);
+    B.qi = S.QH[QHS * t + L.i];
+    B.K0 = S.KR[KRS * t + L.i];
+    B.K1 = S.KR[KRS * t + 6 + L.i];
     B.e1 = a5[L.oe1];
     B.e2 = a5[L.oe2];
-    ld2(S.KP + 10 * t + 2 * L.i, B.K0, B.K1);
-    B.qi = S.QH[QHS * t + L.i];
 }
 __device__ __forceinline__ void load_fwd(const Lds& S, const DLane& L, int t, FwdRec& F) {
     const double* a5 = S.A5 + A5S * t;
-    ld2(S.kk + 2 * t, F.kk0, F.kk1);
-#pragma unroll
-    for (int a = 0; a < 10; a += 2) ld2(S.KP + 10 * t + a, F.K[a], F.K[a + 1]);
+    const double* kr = S.KR + KRS * t + L.kr;
+    ld2(kr, F.K[0], F.K[1]);
+    ld2(kr + 2, F.K[2], F.K[3]);
+    ld2(kr + 4, F.K[4], F.kk);
     F.f0 = a5[L.of0];
     F.f2 = a5[L.of2];
     F.f3 = a5[L.of3];
     F.f4 = a5[L.of4];
 }
+// step t: p = p_{t+1} on entry (stored for phase 2), p_t on exit (t >= 1)
 __device__ __forceinline__ void bwd_step(const Lds& S, const DLane& L, int t, double dt, const BwdRec& B, double& p) {
-    double h0 = B.g0, h1 = B.g1, pn = p;
-    asm("s_nop 1\n\t" DPPF("%0", "%3", "%4", 3) DPPF("%1", "%3", "%4", 4) DPPF("%2", "%3", "%5", 2)
-        DPPF("%2", "%3", "%6", 1) DPPF("%2", "%3", "%7", 0)
-        : "+&v"(h0), "+&v"(h1), "+&v"(pn) : "v"(p), "v"(dt), "v"(B.e2), "v"(B.e1), "v"(L.e0));
-    if (t >= 1) p = fma(B.K0, h0, fma(B.K1, h1, pn + B.qi));
-    const double w0 = h0 * B.si0;
-    const double w1 = (h1 - B.si1 * w0) * B.si2;
-    const double k1 = w1 * B.si2;
-    const double k0 = (w0 - B.si1 * k1) * B.si0;
-    mst2(L.m0, S.kk + 2 * t, k0, k1);
+    S.QR[QRS * (t + 1) + L.ps] = p;
+    if (t >= 1) {
+        double acc = fma(B.K0, B.g0, fma(B.K1, B.g1, B.qi));
+        const double kd0 = B.K0 * dt, kd1 = B.K1 * dt;
+        asm("s_nop 1\n\t" DPPF("%0", "%1", "%2", 3) DPPF("%0", "%1", "%3", 4) DPPF("%0", "%1", "%4", 2)
+            DPPF("%0", "%1", "%5", 1) DPPF("%0", "%1", "%6", 0)
+            : "+&v"(acc) : "v"(p), "v"(kd0), "v"(kd1), "v"(B.e2), "v"(B.e1), "v"(L.e0));
+        p = acc + p;
+    }
+}
+__device__ __forceinline__ void kk_stage(const Lds& S, int t, double dt) {
+    double g0, g1, si0, si1, si2, pad, p3, p4;
+    ld2(S.gh + 2 * t, g0, g1);
+    ld2(S.Si + SIS * t, si0, si1);
+    ld2(S.Si + SIS * t + 2, si2, pad);
+    ld2(S.QR + QRS * (t + 1), p3, p4);
+    const double h0 = fma(p3, dt, g0), h1 = fma(p4, dt, g1);
+    const double w0 = h0 * si0;
+    const double w1 = (h1 - si1 * w0) * si2;
+    const double k1 = w1 * si2;
+    const double k0 = (w0 - si1 * k1) * si0;
+    S.KR[KRS * t + 5] = k0;
+    S.KR[KRS * t + 11] = k1;
 }
 __device__ __forceinline__ void fwd_step(const Lds& S, const DLane& L, int t, const FwdRec& F, double& x) {
-    // u = (K(:,2) x2 + (K(:,0) x0 + (K(:,1) x1 + kk))) + (K(:,3) x3 + K(:,4) x4) and x' = x + J'x with the
-    // terms in the order of the group-uniform recursion (applyA), so the solve rounds as the oracle's
-    double u0 = F.kk0, u1 = F.kk1, v0 = 0.0, v1 = 0.0, xn = x;
-    // operands: %5 x; %6..%15 = (K(0,m), K(1,m)) for m = 0..4; %16..%19 = f0, f2, f3, f4
-    asm("s_nop 1\n\t" DPPF("%0", "%5", "%8", 1) DPPF("%1", "%5", "%9", 1) DPPF("%2", "%5", "%14", 4)
-        DPPF("%3", "%5", "%15", 4) DPPF("%4", "%5", "%19", 4) DPPF("%0", "%5", "%6", 0) DPPF("%1", "%5", "%7", 0)
-        DPPF("%2", "%5", "%12", 3) DPPF("%3", "%5", "%13", 3) DPPF("%4", "%5", "%18", 3)
-        DPPF("%0", "%5", "%10", 2) DPPF("%1", "%5", "%11", 2) DPPF("%4", "%5", "%17", 2)
-        DPPF("%4", "%5", "%16", 0)
-        : "+&v"(u0), "+&v"(u1), "+&v"(v0), "+&v"(v1), "+&v"(xn)
-        : "v"(x), "v"(F.K[0]), "v"(F.K[1]), "v"(F.K[2]), "v"(F.K[3]), "v"(F.K[4]), "v"(F.K[5]), "v"(F.K[6]),
-          "v"(F.K[7]), "v"(F.K[8]), "v"(F.K[9]), "v"(F.f0), "v"(F.f2), "v"(F.f3), "v"(F.f4));
-    u0 = u0 + v0;
-    u1 = u1 + v1;
-    x = fma(L.bu0, u0, fma(L.bu1, u1, xn));
-    mst1(L.m5, S.dX + 5 * (t + 1) + L.i, x);
-    mst2(L.m0, S.dud + 2 * t, u0, u1);
+    // u: lanes 0..3 accumulate row 0 of K (u0), lane 4 row 1 (u1); xa = J'_t x (row i)
+    double u = F.kk, xa = 0.0;
+    asm("s_nop 1\n\t" DPPF("%0", "%2", "%3", 0) DPPF("%1", "%2", "%8", 0) DPPF("%0", "%2", "%4", 1)
+        DPPF("%1", "%2", "%9", 2) DPPF("%0", "%2", "%5", 2) DPPF("%1", "%2", "%10", 3) DPPF("%0", "%2", "%6", 3)
+        DPPF("%1", "%2", "%11", 4) DPPF("%0", "%2", "%7", 4)
+        : "+&v"(u), "+&v"(xa)
+        : "v"(x), "v"(F.K[0]), "v"(F.K[1]), "v"(F.K[2]), "v"(F.K[3]), "v"(F.K[4]), "v"(F.f0), "v"(F.f2),
+          "v"(F.f3), "v"(F.f4));
+    x = fma(L.bu, u, x + xa);
+    S.dX[5 * (t + 1) + L.i] = x;
+    S.dud[2 * t + L.ur] = u;
 }
 
-// NT > 0: the horizon is a compile-time constant and both passes are fully unrolled.
+// NT > 0: the horizon is a compile-time constant and the recursions are fully unrolled.
 template <int NT>
-__device__ __forceinline__ void riccati_solve_lanes(const Lds& S, int Nrt, double dt, int gl) {
-    const int N = NT > 0 ? NT : Nrt;
+__device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, int gl) {
     const DLane L = dlane(gl, dt);
     double p = S.QH[QHS * N + L.i];
 #ifdef MPC_SOLVE_LOOP
@@ -729,8 +704,12 @@ __device__ __forceinline__ void riccati_solve_lanes(const Lds& S, int Nrt, doubl
             if (--t < 0) break;
         }
     }
+}
+template <int NT>
+__device__ __forceinline__ void solve_fwd_lanes(const Lds& S, int N, double dt, int gl) {
+    const DLane L = dlane(gl, dt);
     double x = 0.0;
-    mst1(L.m5, S.dX + L.i, 0.0);
+    S.dX[L.i] = 0.0;
 #ifdef MPC_SOLVE_LOOP
     if constexpr (false) {
 #else
@@ -763,9 +742,15 @@ __device__ __forceinline__ void riccati_solve_lanes(const Lds& S, int Nrt, doubl
         }
     }
 }
+// the recursions run on lanes 0..4 of each group (exec narrowed), the kk phase on lanes 0..N-1
 template <int NT>
 __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
-    if (!MPC_EXEC5 || gl < 5) riccati_solve_lanes<NT>(S, Nrt, dt, gl);
+    const int N = NT > 0 ? NT : Nrt;
+    if (gl < 5) solve_bwd_lanes<NT>(S, N, dt, gl);
+    wave_sync();
+    if (gl < N) kk_stage(S, gl, dt);
+    wave_sync();
+    if (gl < 5) solve_fwd_lanes<NT>(S, N, dt, gl);
     wave_sync();
 }
 
