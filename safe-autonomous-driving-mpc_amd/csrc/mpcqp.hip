@@ -408,6 +408,8 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // with early-clobber accumulators, so no accumulator shares a register with a source.  The leading
 // s_nop 1 covers the VALU-write -> DPP-read hazard (2 wait states) of the sources.
 #define DPPF(d, s, c, L) "v_fmac_f64_dpp " d ", " s ", " c " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
+// dst -= src@L * c (DPP source negation modifier)
+#define DPPFN(d, s, c, L) "v_fmac_f64_dpp " d ", -" s ", " c " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
 
 
 // Per-lane constants of the distributed recursions.  A_t = I + J'_t with J' nonzero in rows 0..2 only:
@@ -477,17 +479,13 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
     double s00 = F.r0, s01 = 0.0, s11 = F.r1;
     asm("s_nop 1\n\t" DPPF("%0", "%3", "%5", 3) DPPF("%1", "%4", "%5", 3) DPPF("%2", "%4", "%5", 4)
         : "+&v"(s00), "+&v"(s01), "+&v"(s11) : "v"(pr[3]), "v"(pr[4]), "v"(dt2));
-    if (!(s00 > 0.0)) s00 = 1e-300 + fabs(s00);
+    // pivot floors: never active in practice (s00 >= Rt >= 2 w_u1 > 0); a NaN pivot is floored too, the
+    // NaN still reaches P and K through V and M
+    s00 = fmax(s00, 1e-300);
     const double il00 = frsqrt(s00), l10 = s01 * il00;
-    double r11 = s11 - l10 * l10;
-    if (!(r11 > 1e-14 * s11)) r11 = 1e-14 * fabs(s11) + 1e-300;
+    const double r11 = fmax(s11 - l10 * l10, 1e-14 * s11);
     const double il11 = frsqrt(r11);
     const double c0 = dt * il00, c1 = dt * il11, c2 = -l10 * il11;
-    // V3 = M(3,i), V4 = M(4,i) = P(i,{3,4}) + sum_l J'(l,i) P(l,{3,4})
-    double v3 = pr[3], v4 = pr[4];
-    asm("s_nop 1\n\t" DPPF("%0", "%2", "%4", 2) DPPF("%1", "%3", "%4", 2) DPPF("%0", "%2", "%5", 1)
-        DPPF("%1", "%3", "%5", 1) DPPF("%0", "%2", "%6", 0) DPPF("%1", "%3", "%6", 0)
-        : "+&v"(v3), "+&v"(v4) : "v"(pr[3]), "v"(pr[4]), "v"(F.e2), "v"(F.e1), "v"(L.e0));
     // row i of M = P A (local)
     double m[5];
     m[0] = fma(pr[2], a20, pr[0]);
@@ -495,19 +493,29 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
     m[2] = fma(pr[1], a12, pr[2]);
     m[3] = fma(pr[2], a23, pr[3]);
     m[4] = fma(pr[0], dt, fma(pr[1], a14, fma(pr[2], a24, pr[4])));
-    double am[5] = {m[0], m[1], m[2], m[3], m[4]};
+    // row i of A'M = M(i,:) + sum_l J'(l,i) M(l,:), and V3 = M(3,i), V4 = M(4,i) = P(i,{3,4}) +
+    // sum_l J'(l,i) P(l,{3,4}), all in place.  Source lane l only changes in the broadcast of a lane l'
+    // with J'(l',l) != 0; with J' nonzero at (0,4), (1,2), (1,4), (2,0), (2,3), (2,4) the order l = 0, 2, 1
+    // reads every source lane before its own update (a zero coefficient leaves a value unchanged).
+    // The same register is written and then broadcast 7 instructions later (the DPP hazard needs 2).
+    double v3 = pr[3], v4 = pr[4];
     if (upd) {
-        // row i of A'M = M(i,:) + sum_l J'(l,i) M(l,:)
-#define DPP_AM(L, c)                                                                                        \
-        asm("s_nop 1\n\t" DPPF("%0", "%5", "%10", L) DPPF("%1", "%6", "%10", L) DPPF("%2", "%7", "%10", L) \
-            DPPF("%3", "%8", "%10", L) DPPF("%4", "%9", "%10", L)                                            \
-            : "+&v"(am[0]), "+&v"(am[1]), "+&v"(am[2]), "+&v"(am[3]), "+&v"(am[4])                           \
-            : "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]), "v"(m[4]), "v"(c))
-        DPP_AM(2, F.e2);
-        DPP_AM(1, F.e1);
-        DPP_AM(0, L.e0);
-#undef DPP_AM
+        asm("s_nop 1\n\t"
+            DPPF("%0", "%0", "%7", 0) DPPF("%1", "%1", "%7", 0) DPPF("%2", "%2", "%7", 0) DPPF("%3", "%3", "%7", 0)
+            DPPF("%4", "%4", "%7", 0) DPPF("%5", "%5", "%7", 0) DPPF("%6", "%6", "%7", 0)
+            DPPF("%0", "%0", "%8", 2) DPPF("%1", "%1", "%8", 2) DPPF("%2", "%2", "%8", 2) DPPF("%3", "%3", "%8", 2)
+            DPPF("%4", "%4", "%8", 2) DPPF("%5", "%5", "%8", 2) DPPF("%6", "%6", "%8", 2)
+            DPPF("%0", "%0", "%9", 1) DPPF("%1", "%1", "%9", 1) DPPF("%2", "%2", "%9", 1) DPPF("%3", "%3", "%9", 1)
+            DPPF("%4", "%4", "%9", 1) DPPF("%5", "%5", "%9", 1) DPPF("%6", "%6", "%9", 1)
+            : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]), "+v"(m[3]), "+v"(m[4]), "+v"(v3), "+v"(v4)
+            : "v"(L.e0), "v"(F.e2), "v"(F.e1));
+    } else {
+        asm("s_nop 1\n\t" DPPF("%0", "%0", "%2", 0) DPPF("%1", "%1", "%2", 0) "s_nop 1\n\t"
+            DPPF("%0", "%0", "%3", 2) DPPF("%1", "%1", "%3", 2) "s_nop 1\n\t"
+            DPPF("%0", "%0", "%4", 1) DPPF("%1", "%1", "%4", 1)
+            : "+v"(v3), "+v"(v4) : "v"(L.e0), "v"(F.e2), "v"(F.e1));
     }
+    double* am = m;
     const double w0 = c0 * v3;
     const double w1 = fma(c1, v4, c2 * w0);
     const double K1 = -w1 * il11;
@@ -521,12 +529,11 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
     S.Si[SIS * t + 2] = il11;
     if (upd) {
         // P(i,j) = A'M(i,j) - W1_i W1_j - W0_i W0_j + Qt(i,j)
-        const double nw0 = -w0, nw1 = -w1;
-        asm("s_nop 1\n\t" DPPF("%0", "%5", "%7", 0) DPPF("%1", "%5", "%7", 1) DPPF("%2", "%5", "%7", 2)
-            DPPF("%3", "%5", "%7", 3) DPPF("%4", "%5", "%7", 4) DPPF("%0", "%6", "%8", 0) DPPF("%1", "%6", "%8", 1)
-            DPPF("%2", "%6", "%8", 2) DPPF("%3", "%6", "%8", 3) DPPF("%4", "%6", "%8", 4)
+        asm("s_nop 1\n\t" DPPFN("%0", "%5", "%5", 0) DPPFN("%1", "%5", "%5", 1) DPPFN("%2", "%5", "%5", 2)
+            DPPFN("%3", "%5", "%5", 3) DPPFN("%4", "%5", "%5", 4) DPPFN("%0", "%6", "%6", 0) DPPFN("%1", "%6", "%6", 1)
+            DPPFN("%2", "%6", "%6", 2) DPPFN("%3", "%6", "%6", 3) DPPFN("%4", "%6", "%6", 4)
             : "+&v"(am[0]), "+&v"(am[1]), "+&v"(am[2]), "+&v"(am[3]), "+&v"(am[4])
-            : "v"(w1), "v"(w0), "v"(nw1), "v"(nw0));
+            : "v"(w1), "v"(w0));
         pr[0] = am[0] + F.q[0];
         pr[1] = am[1] + F.q[1];
         pr[2] = am[2] + F.q[2];
