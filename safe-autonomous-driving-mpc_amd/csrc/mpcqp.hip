@@ -160,7 +160,12 @@ struct Lds {
     double* zs;    // [N][2]    control terms zc + za
     double* ub;    // [N][2]    linearisation point
     double* kap;   // [N+1]     k_ref(xbar_k) (setup); aliases QH after Xr
+    double* AC;    // [N][5][6] closed-loop rows (A_t + B K_t)(i,:) and (B kk_t)_i of the forward solve
+                   //           (kernels with acl_on only; rows 0..2 are A's, written at setup)
 };
+// the forward solve reads closed-loop rows (AC) in the horizon-specialised kernels and for GL = 64; the
+// runtime-horizon GL <= 32 kernels keep the K-row form (AC would cost them an occupancy step at N ~ 30)
+__host__ __device__ constexpr bool acl_on(int GL, int NT) { return NT > 0 || GL == 64; }
 // At convergence the separate dual-residual terms (yc, ya, zc, za) go to a scratch in QR rows 0..2
 // (the factorisation is dead then; the polish rewrites those rows): yc of stage k at QR[k][0..3],
 // ya at QR[k][4..7], zc / za of control t at QR[t][8..9] / QR[t][10..11].
@@ -169,17 +174,18 @@ struct Lds {
 #define DQ_ZC 8
 #define DQ_ZA 10
 
-__host__ __device__ inline int lds_doubles(int N) {
+__host__ __device__ inline int lds_doubles(int N, bool acl) {
     int NP = N + 1;
-    int n = N * A5S + NP * 6 + NP * QRS + N * 2 + N * KRS + N * SIS + NP * QHS + N * 2 + N * 2 + NP * 4 +
+    int n = (acl ? N * 30 : 0) + N * A5S + NP * 6 + NP * QRS + N * 2 + N * KRS + N * SIS + NP * QHS + N * 2 + N * 2 + NP * 4 +
             N * 2 + N * 2 + NP * 5;
     return (n + 1) & ~1;     // groups stay 16-B aligned
 }
 
-__device__ inline Lds carve(double* p, int N) {
+__device__ inline Lds carve(double* p, int N, bool acl) {
     Lds L;
     int NP = N + 1;
     // even-sized arrays first (16-B aligned starts), the odd-sized ones last
+    L.AC = p; p += acl ? N * 30 : 0;
     L.A5 = p; p += N * A5S;
     L.cst = p; p += NP * 6;
     L.QR = p; p += NP * QRS;
@@ -661,6 +667,54 @@ __device__ __forceinline__ void kk_stage(const Lds& S, int t, double dt) {
     S.KR[KRS * t + 5] = k0;
     S.KR[KRS * t + 11] = k1;
 }
+// closed-loop rows 3, 4 of stage t for the forward solve: e_{3+r}' + dt K_t(r,:) and dt kk_r
+__device__ __forceinline__ void ac_rows(const Lds& S, int t, double dt) {
+    const double* kr = S.KR + KRS * t;
+    double* ac = S.AC + 30 * t + 18;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        double k[6];
+#pragma unroll
+        for (int m = 0; m < 6; m += 2) ld2(kr + 6 * r + m, k[m], k[m + 1]);
+#pragma unroll
+        for (int m = 0; m < 5; ++m) ac[6 * r + m] = (m == 3 + r) ? fma(dt, k[m], 1.0) : dt * k[m];
+        ac[6 * r + 5] = dt * k[5];
+    }
+}
+// u_t = kk_t + K_t x_t after the closed-loop forward solve (stage-parallel; the accumulation order of
+// the K-row forward step)
+__device__ __forceinline__ void u_stage(const Lds& S, int t) {
+    const double* kr = S.KR + KRS * t;
+    const double* x = S.dX + 5 * t;
+    double xv[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m) xv[m] = x[m];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        double k[6];
+#pragma unroll
+        for (int m = 0; m < 6; m += 2) ld2(kr + 6 * r + m, k[m], k[m + 1]);
+        double u = k[5];
+#pragma unroll
+        for (int m = 0; m < 5; ++m) u = fma(xv[m], k[m], u);
+        S.dud[2 * t + r] = u;
+    }
+}
+struct AclRec { double c[5], d; };
+__device__ __forceinline__ void load_acl(const Lds& S, const DLane& L, int t, AclRec& F) {
+    const double* ac = S.AC + 30 * t + 6 * L.i;
+    ld2(ac, F.c[0], F.c[1]);
+    ld2(ac + 2, F.c[2], F.c[3]);
+    ld2(ac + 4, F.c[4], F.d);
+}
+// x_{t+1}(i) = sum_m Acl_t(i,m) x_m + (B kk_t)_i: one chain of five broadcast FMAs
+__device__ __forceinline__ void acl_step(const Lds& S, const DLane& L, int t, AclRec& F, double& x) {
+    asm("s_nop 1\n\t" DPPF("%0", "%1", "%2", 0) DPPF("%0", "%1", "%3", 1) DPPF("%0", "%1", "%4", 2)
+        DPPF("%0", "%1", "%5", 3) DPPF("%0", "%1", "%6", 4)
+        : "+&v"(F.d) : "v"(x), "v"(F.c[0]), "v"(F.c[1]), "v"(F.c[2]), "v"(F.c[3]), "v"(F.c[4]));
+    x = F.d;
+    S.dX[5 * (t + 1) + L.i] = x;
+}
 __device__ __forceinline__ void fwd_step(const Lds& S, const DLane& L, int t, const FwdRec& F, double& x) {
     // u: lanes 0..3 accumulate row 0 of K (u0), lane 4 row 1 (u1); xa = J'_t x (row i)
     double u = F.kk, xa = 0.0;
@@ -713,6 +767,39 @@ __device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, 
     }
 }
 template <int NT>
+__device__ __forceinline__ void solve_acl_lanes(const Lds& S, int N, double dt, int gl) {
+    const DLane L = dlane(gl, dt);
+    double x = 0.0;
+    S.dX[L.i] = 0.0;
+    if constexpr (NT > 0) {
+        AclRec buf[2];
+        load_acl(S, L, 0, buf[0]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            sched_fence();
+            load_acl(S, L, t + 1 < NT ? t + 1 : t, buf[(t + 1) & 1]);
+            sched_fence();
+            acl_step(S, L, t, buf[t & 1], x);
+        }
+    } else {
+        AclRec A, B;
+        load_acl(S, L, 0, A);
+        int t = 0;
+        while (true) {
+            sched_fence();
+            load_acl(S, L, t + 1 < N ? t + 1 : t, B);
+            sched_fence();
+            acl_step(S, L, t, A, x);
+            if (++t >= N) break;
+            sched_fence();
+            load_acl(S, L, t + 1 < N ? t + 1 : t, A);
+            sched_fence();
+            acl_step(S, L, t, B, x);
+            if (++t >= N) break;
+        }
+    }
+}
+template <int NT>
 __device__ __forceinline__ void solve_fwd_lanes(const Lds& S, int N, double dt, int gl) {
     const DLane L = dlane(gl, dt);
     double x = 0.0;
@@ -749,15 +836,25 @@ __device__ __forceinline__ void solve_fwd_lanes(const Lds& S, int N, double dt, 
         }
     }
 }
-// the recursions run on lanes 0..4 of each group (exec narrowed), the kk phase on lanes 0..N-1
-template <int NT>
+// the recursions run on lanes 0..4 of each group (exec narrowed), the stage phases on lanes 0..N-1.
+// ACL: the forward solve runs on closed-loop rows (built with kk) and u follows stage-parallel.
+template <int NT, bool ACL>
 __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
     const int N = NT > 0 ? NT : Nrt;
     if (gl < 5) solve_bwd_lanes<NT>(S, N, dt, gl);
     wave_sync();
-    if (gl < N) kk_stage(S, gl, dt);
+    if (gl < N) {
+        kk_stage(S, gl, dt);
+        if (ACL) ac_rows(S, gl, dt);
+    }
     wave_sync();
-    if (gl < 5) solve_fwd_lanes<NT>(S, N, dt, gl);
+    if (ACL) {
+        if (gl < 5) solve_acl_lanes<NT>(S, N, dt, gl);
+        wave_sync();
+        if (gl < N) u_stage(S, gl);
+    } else {
+        if (gl < 5) solve_fwd_lanes<NT>(S, N, dt, gl);
+    }
     wave_sync();
 }
 
@@ -898,7 +995,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     const double dt = Pr.dt;
     const double rho = Pr.rho;
     const double hL = Pr.L / 2.0;
-    Lds S = carve(smem + (size_t)grp * lds_doubles(N), N);
+    constexpr bool ACL = acl_on(GL, NT);
+    Lds S = carve(smem + (size_t)grp * lds_doubles(N, ACL), N, ACL);
 
     double x0[5];
 #pragma unroll
@@ -973,6 +1071,15 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             S.A5[A5S * gl + 5] = dt;      // a04, read by the per-lane gathers (DLane)
             S.A5[A5S * gl + 6] = 0.0;     // the gathers' zero slot
             S.A5[A5S * gl + 7] = 0.0;
+            if (ACL) {
+                // rows 0..2 of the forward solve's closed-loop matrix are A_t's (B has rows 3, 4 only)
+                double* ac = S.AC + 30 * gl;
+                const double a12 = dt * x[4], a14 = dt * x[2], a20 = dt * (-x[4] * dk), a23 = dt * x[4];
+                const double a24 = dt * (x[3] - refk[3]);
+                ac[0] = 1.0; ac[1] = 0.0; ac[2] = 0.0; ac[3] = 0.0; ac[4] = dt; ac[5] = 0.0;
+                ac[6] = 0.0; ac[7] = 1.0; ac[8] = a12; ac[9] = 0.0; ac[10] = a14; ac[11] = 0.0;
+                ac[12] = a20; ac[13] = 0.0; ac[14] = 1.0; ac[15] = a23; ac[16] = a24; ac[17] = 0.0;
+            }
         }
         if (gl <= N) {
             // the k row of QR is structurally zero (no cost or row touches k); the k entry of QH is
@@ -1273,7 +1380,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 }
                 wave_sync();
                 PROF(6)
-                riccati_solve<NTR>(S, N, dt, gl);
+                riccati_solve<NTR, ACL>(S, N, dt, gl);
                 PROF(7)
                 // row directions and the largest feasible step
                 double dx4[4];
@@ -1476,7 +1583,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         S.gh[2 * (k - 1) + 1] = g1 - fma(R1, pu1, R1 * S.ub[2 * (k - 1) + 1]);
                     }
                     wave_sync();
-                    riccati_solve<NTR>(S, N, dt, gl);
+                    riccati_solve<NTR, ACL>(S, N, dt, gl);
                     {
                         double dx4[4];
 #pragma unroll
@@ -1982,13 +2089,13 @@ extern "C" void mpc_destroy(mpc_ctx* c) {
 static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, const double* obs, const int* n_obs,
                         const double* ubar, double* u0, double* U, double* Xpred, int* status, int* iters,
                         hipStream_t st) {
-    size_t lds = sizeof(double) * (size_t)lds_doubles(kp.N);
-    if (lds > 160 * 1024) return fail(MPC_E_ARG, "horizon too long for LDS");
     // G = 64 / GL instances per wavefront: the smallest lane group holding the N + 1 stages
     const int* nob = obs ? n_obs : nullptr;
     const int GL = kp.N + 1 <= 16 ? 16 : (kp.N + 1 <= 32 ? 32 : 64);
     const int G = WAVE / GL;
-    const size_t lds_wave = lds * G;
+    const bool nt20 = kp.N == 20 && !MPC_NO_NT20;
+    const size_t lds_wave = sizeof(double) * (size_t)lds_doubles(kp.N, acl_on(GL, nt20 ? 20 : 0)) * G;
+    if (lds_wave > 160 * 1024) return fail(MPC_E_ARG, "horizon too long for LDS");
     const dim3 grid((B + G - 1) / G);
     // Two-phase launch (MODE_XO then MODE_IPM) for single-QP solves with the crossover on; the work
     // list lives in the context (one list per context: a context is not re-entrant, include/mpcqp.h).
@@ -2011,7 +2118,7 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     // horizon-specialised kernels for the BASELINE horizons that pay for their code size (N = 20)
 #define MPC_LAUNCH_GL(MODEV)                                                                   \
     do {                                                                                       \
-        if (kp.N == 20 && !MPC_NO_NT20) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 20); else MPC_LAUNCH(32, false, MODEV, 20); } \
+        if (nt20) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 20); else MPC_LAUNCH(32, false, MODEV, 20); } \
         else if (GL == 16) { if (with_obs) MPC_LAUNCH(16, true, MODEV, 0); else MPC_LAUNCH(16, false, MODEV, 0); } \
         else if (GL == 32) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 0); else MPC_LAUNCH(32, false, MODEV, 0); } \
         else { if (with_obs) MPC_LAUNCH(64, true, MODEV, 0); else MPC_LAUNCH(64, false, MODEV, 0); } \
