@@ -1388,7 +1388,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 for (int a = 0; a < 4; ++a) dx4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
                 const double dd0 = live ? S.dud[2 * (k - 1)] : 0.0, dd1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
                 double dsv[NR], dlv[NR], dxv[NR], dnv[NR], dsb[NBOX], dlb[NBOX];
-                double amax = 1.0;
+                // ratio tests as rmax = max(1, max_j -d_j / x_j); the step to the boundary is 1 / rmax.
+                // The reciprocals of lam, nu (rows) and lam (boxes) are the barrier weights' il, inu,
+                // ilb; s, xi (rows) and s (boxes) take the approximate v_rcp_f64 (enough for a step
+                // length).  A product and a max per term (no compare, select or NaN canonicalisation).
+                double rmax = 1.0;
 #pragma unroll
                 for (int j = 0; j < NR; ++j) {
                     const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
@@ -1405,11 +1409,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     dlv[j] = on ? dl : 0.0;
                     dxv[j] = on ? dxi : 0.0;
                     dnv[j] = on ? dn : 0.0;
-                    // ratio tests: the approximate reciprocal is enough for a step length
-                    if (dsv[j] < 0.0) amax = fmin(amax, -rs[j] * __builtin_amdgcn_rcp(dsv[j]));
-                    if (dlv[j] < 0.0) amax = fmin(amax, -rl[j] * __builtin_amdgcn_rcp(dlv[j]));
-                    if (dxv[j] < 0.0) amax = fmin(amax, -rxi[j] * __builtin_amdgcn_rcp(dxv[j]));
-                    if (dnv[j] < 0.0) amax = fmin(amax, -rnu[j] * __builtin_amdgcn_rcp(dnv[j]));
+                    rmax = fmax(rmax, -dsv[j] * __builtin_amdgcn_rcp(rs[j]));
+                    rmax = fmax(rmax, -dlv[j] * il[j]);
+                    rmax = fmax(rmax, -dxv[j] * __builtin_amdgcn_rcp(rxi[j]));
+                    rmax = fmax(rmax, -dnv[j] * inu[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j) {
@@ -1420,10 +1423,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double ds = -fma(sb[j], dl, r4) * ilb[j];
                     dsb[j] = ds;
                     dlb[j] = dl;
-                    if (dsb[j] < 0.0) amax = fmin(amax, -sb[j] * __builtin_amdgcn_rcp(dsb[j]));
-                    if (dlb[j] < 0.0) amax = fmin(amax, -lb[j] * __builtin_amdgcn_rcp(dlb[j]));
+                    rmax = fmax(rmax, -dsb[j] * __builtin_amdgcn_rcp(sb[j]));
+                    rmax = fmax(rmax, -dlb[j] * ilb[j]);
                 }
-                amax = Q.min(live ? amax : 1.0);
+                const double amax = __builtin_amdgcn_rcp(Q.max(live ? rmax : 1.0));
                 // complementarity after the step (pass 0: at the full affine step length)
                 const double a_try = (pass == 0) ? amax : fmin(1.0, TAU * amax);
                 double ca = 0.0;
