@@ -1,0 +1,96 @@
+// Cycle cost of the Riccati phases of the product kernel in isolation (one wavefront, two N = 20
+// groups, synthetic but well-conditioned stage data).  Includes the product source, so it times the
+// exact device code that ships.  s_memtime cycles per call, averaged over REP calls.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o phase_micro phase_micro.hip
+#include "../../safe-autonomous-driving-mpc_amd/csrc/mpcqp.hip"
+#include <cstdio>
+
+#define NTP 20
+#define REP 16
+
+__global__ void __launch_bounds__(64) probe(long long* cyc, double* out) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int ln = threadIdx.x, grp = ln / 32, gl = ln % 32;
+    const int N = NTP;
+    constexpr bool ACL = true;
+    Lds S = carve(smem + (size_t)grp * lds_doubles(N, ACL), N, ACL);
+    const double dt = 0.2;
+    // synthetic stage data: A from a plausible linearisation, SPD stage Hessians, unit control weights
+    if (gl < N) {
+        double* a = S.A5 + A5S * gl;
+        a[0] = dt * 10.0; a[1] = dt * 0.01; a[2] = -dt * 0.001 * gl; a[3] = dt * 10.0; a[4] = dt * 0.02;
+        a[5] = dt; a[6] = 0.0; a[7] = 0.0;
+        double* ac = S.AC + 30 * gl;
+        ac[0] = 1.0; ac[1] = 0.0; ac[2] = 0.0; ac[3] = 0.0; ac[4] = dt; ac[5] = 0.0;
+        ac[6] = 0.0; ac[7] = 1.0; ac[8] = a[0]; ac[9] = 0.0; ac[10] = a[1]; ac[11] = 0.0;
+        ac[12] = a[2]; ac[13] = 0.0; ac[14] = 1.0; ac[15] = a[3]; ac[16] = a[4]; ac[17] = 0.0;
+        S.Rt[2 * gl] = 1.0 + 1e3 * (gl & 1);
+        S.Rt[2 * gl + 1] = 1.0 + 1e2 * (gl % 3);
+        S.gh[2 * gl] = 0.1 * gl;
+        S.gh[2 * gl + 1] = -0.05 * gl;
+    }
+    if (gl <= N) {
+        double* q = S.QR + QRS * gl;
+        for (int r = 0; r < 20; ++r) q[r] = 0.0;
+        // rows (s,d,o,k,v) x cols (s,d,o,v): diagonal-dominant
+        q[0] = 1.0; q[5] = 10.0 + 1e4 * (gl % 4 == 0); q[6] = 0.5; q[9] = 0.5; q[10] = 10.0; q[19] = 5.0 + 1e6 * (gl % 5 == 0);
+        double* h = S.QH + QHS * gl;
+        h[0] = 0.01 * gl; h[1] = -0.2; h[2] = 0.1; h[3] = 0.0; h[4] = 0.3; h[5] = 0.0;
+    }
+    wave_sync();
+    long long t0, t1, acc_f = 0, acc_s = 0, acc_b = 0, acc_k = 0, acc_w = 0, acc_u = 0;
+    for (int r = 0; r < REP; ++r) {
+        t0 = __builtin_amdgcn_s_memtime();
+        riccati_factor<NTP>(S, N, dt, gl);
+        t1 = __builtin_amdgcn_s_memtime();
+        acc_f += t1 - t0;
+        t0 = __builtin_amdgcn_s_memtime();
+        riccati_solve<NTP, ACL>(S, N, dt, gl);
+        t1 = __builtin_amdgcn_s_memtime();
+        acc_s += t1 - t0;
+        // the solve's phases one by one
+        t0 = __builtin_amdgcn_s_memtime();
+        if (gl < 5) solve_bwd_lanes<NTP>(S, N, dt, gl);
+        wave_sync();
+        t1 = __builtin_amdgcn_s_memtime();
+        acc_b += t1 - t0;
+        t0 = t1;
+        if (gl < N) { kk_stage(S, gl, dt); ac_rows(S, gl, dt); }
+        wave_sync();
+        t1 = __builtin_amdgcn_s_memtime();
+        acc_k += t1 - t0;
+        t0 = t1;
+        if (gl < 5) solve_acl_lanes<NTP>(S, N, dt, gl);
+        wave_sync();
+        t1 = __builtin_amdgcn_s_memtime();
+        acc_w += t1 - t0;
+        t0 = t1;
+        if (gl < N) u_stage(S, gl);
+        wave_sync();
+        t1 = __builtin_amdgcn_s_memtime();
+        acc_u += t1 - t0;
+    }
+    if (ln == 0) {
+        cyc[0] = acc_f / REP; cyc[1] = acc_s / REP; cyc[2] = acc_b / REP; cyc[3] = acc_k / REP;
+        cyc[4] = acc_w / REP; cyc[5] = acc_u / REP;
+    }
+    out[ln] = S.dX[5 * N + (gl % 5)] + S.dud[2 * (N - 1)];
+}
+
+int main() {
+    long long* c;
+    double* o;
+    (void)hipMalloc(&c, 16 * sizeof(long long));
+    (void)hipMalloc(&o, 64 * sizeof(double));
+    const size_t lds = 2 * sizeof(double) * (size_t)lds_doubles(NTP, true);
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(probe, dim3(1), dim3(64), lds, 0, c, o);
+    (void)hipDeviceSynchronize();
+    long long h[16];
+    double ho[64];
+    (void)hipMemcpy(h, c, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(ho, o, sizeof(ho), hipMemcpyDeviceToHost);
+    printf("N=%d cycles per call: factor %lld (%.0f/stage)  solve %lld | bwd %lld (%.0f/stage)  kk+rows %lld  "
+           "fwd %lld (%.0f/stage)  u %lld   [check %.6e]\n",
+           NTP, h[0], (double)h[0] / NTP, h[1], h[2], (double)h[2] / NTP, h[3], h[4], (double)h[4] / NTP, h[5], ho[0]);
+    return 0;
+}
