@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--inflight", type=int, default=4, metavar="K",
+                    help="secondary serving leg: K independent batches of the same shape in flight on K streams "
+                         "(one solver context each); reported as 'inflight', never as 'value' (0: skip)")
     ap.add_argument("--closed-loop", type=int, default=0, metavar="B",
                     help="also run B egos through the device closed loop (mpc_closed_loop, SURVEY 8(f)1) on the "
                          "config's trajectory and FSM preset and report closed-loop ego-steps/s")
@@ -177,6 +180,8 @@ def main():
                                  "PMC HBM bytes per step (profiles/pmc_hbm_bytes.json)",
                          "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
         }
+        if args.inflight > 1:
+            out["inflight"] = inflight(args.inflight, args.steps, wb, B, N, mo, X, U, dev, world)
         if args.closed_loop:
             out["closed_loop"] = closed_loop(args.config, args.closed_loop, N, local)
         if not args.no_cpu:
@@ -185,6 +190,55 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def inflight(K, steps, wb, B, N, mo, X, U, dev, world):
+    """Serving leg (not the headline `value`): K independent batches of B solves in flight at once, one
+    solver context and one HIP stream each, `steps` rounds of K submissions.  A single batch leaves SIMDs idle
+    while its slowest interior-point instance finishes (tail bound); independent batches on
+    other streams fill them.  Every batch is complete and checked (its status/iteration telemetry must equal
+    the sequential batch's); rank 0 only, after the headline timing."""
+    import numpy as np
+    import torch
+    import mpcqp
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    ptr = lambda x: 0 if x is None else x.data_ptr()
+    x0 = t(wb["x0"])
+    obs = t(wb["obs"]) if wb["obs"] is not None else None
+    nob = t(wb["n_obs"], torch.int32) if wb["n_obs"] is not None else None
+    ctx = []
+    for _ in range(K):
+        slv = mpcqp.Solver(X, U, mpcqp.default_params(N=N, max_obs=mo), device=dev.index)
+        o = dict(u0=torch.empty((B, 2), dtype=torch.float64, device=dev),
+                 U=torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+                 X=torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev),
+                 st=torch.empty(B, dtype=torch.int32, device=dev), it=torch.empty(B, dtype=torch.int32, device=dev))
+        ctx.append((slv, torch.cuda.Stream(dev), o))
+
+    def submit(slv, stream, o):
+        slv.solve_batch_device(B, ptr(x0), ptr(obs), ptr(nob), 0, ptr(o["u0"]), ptr(o["U"]), ptr(o["X"]),
+                               ptr(o["st"]), ptr(o["it"]), stream=stream.cuda_stream)
+
+    cur = torch.cuda.current_stream(dev)
+    for c in ctx:                                   # warm-up, and inputs visible to every stream
+        c[1].wait_stream(cur)
+        submit(*c)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for c in ctx:
+            submit(*c)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    st0, it0 = ctx[0][2]["st"].cpu().numpy(), ctx[0][2]["it"].cpu().numpy()
+    same = all(np.array_equal(c[2]["st"].cpu().numpy(), st0) and np.array_equal(c[2]["it"].cpu().numpy(), it0)
+               and torch.equal(c[2]["U"], ctx[0][2]["U"]) for c in ctx[1:])
+    for c in ctx:
+        c[0].close()
+    return {"batches_in_flight": K, "value_per_gpu": K * steps * B / dt, "unit": "solves/s",
+            "ms_per_batch": dt * 1e3 / (K * steps), "batches": K * steps, "outputs_identical_across_streams": same,
+            "note": "secondary serving measurement on rank 0 (per GPU): independent batches of the same shape on "
+                    "K streams; the headline value above is one batch at a time"}
 
 
 def closed_loop(config, B, N, device, sqp_iters=4):

@@ -52,6 +52,9 @@ struct DevTable {
     int T, Tu;
     double smax;
     double last[5];    // X_ref[-1] verbatim (trajectory_loader.py:90-91)
+    const int* bidx;   // [nb + 1] bucket index of s: bidx[g] = lower_bound(s, s0 + g h)
+    int nb;
+    double s0, ibh;    // s[0], 1 / h
 };
 
 struct KParams {
@@ -85,12 +88,18 @@ __device__ __forceinline__ void wave_sync() { __syncthreads(); }
 // ------------------------------------------------------------------------------------------
 // reference signal: scipy interp1d 'linear' + extrapolate (scipy _interpolate.py:457-483)
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int seg(const double* __restrict__ x, int n, double v) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (x[mid] < v) lo = mid + 1; else hi = mid;
-    }
+// interval of v in the table's s column (n <= T: a prefix of it), i.e. scipy's searchsorted
+// (lower bound) clamped to [1, n - 1].  The lower bound is found from the bucket index (one load) and
+// corrected by stepping, so the result is the binary search's exactly while the dependent chain is
+// ~2 L2 loads instead of log2(T) (every instance looks up ~4 N times)
+__device__ __forceinline__ int seg_t(const DevTable& t, int n, double v) {
+    double gf = (v - t.s0) * t.ibh;
+    gf = gf > 0.0 ? gf : 0.0;                       // also maps NaN to bucket 0
+    const int g = gf < (double)(t.nb - 1) ? (int)gf : t.nb - 1;
+    int lo = t.bidx[g];
+    while (lo < t.T && t.s[lo] < v) ++lo;
+    while (lo > 0 && !(t.s[lo - 1] < v)) --lo;
+    lo = lo < n ? lo : n;
     lo = lo < 1 ? 1 : lo;
     lo = lo > n - 1 ? n - 1 : lo;
     return lo;
@@ -109,7 +118,7 @@ __device__ void get_state(const DevTable& t, double s, double* out, double* sl) 
         if (sl) sl[0] = sl[1] = sl[2] = sl[3] = 0.0;
         return;
     }
-    int i = seg(t.s, t.T, s);
+    int i = seg_t(t, t.T, s);
     out[0] = s;
     out[1] = lin(t.s, t.d, i, s);
     out[2] = lin(t.s, t.o, i, s);
@@ -125,7 +134,7 @@ __device__ void get_state(const DevTable& t, double s, double* out, double* sl) 
 // get_control (trajectory_loader.py:95-102)
 __device__ void get_control(const DevTable& t, double s, double* out) {
     if (s >= t.smax) { out[0] = 0.0; out[1] = 0.0; return; }
-    int i = seg(t.s, t.Tu, s);
+    int i = seg_t(t, t.Tu, s);
     out[0] = lin(t.s, t.u1, i, s);
     out[1] = lin(t.s, t.u2, i, s);
 }
@@ -1314,7 +1323,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int j = 0; j < NBOX; ++j) pbv[j] = 0.0;
             double sig = 0.0;
             bool breakdown = false;
+#ifdef MPC_PASS_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
             for (int pass = 0; pass < 3; ++pass) {
                 // pass 0: affine predictor; 1: Mehrotra corrector; 2: plain centred direction, taken when
                 // the corrector would not reduce complementarity (oracle: comp_after > comp)
@@ -1839,7 +1852,7 @@ __global__ void mpc_pose_kernel(DevTable tab, int n, const double* __restrict__ 
     if (i >= n) return;
     double si = s[i];
     if (si > tab.smax) si = tab.smax;
-    const int j = seg(tab.s, tab.T, si);
+    const int j = seg_t(tab, tab.T, si);
     const double xr = lin(tab.s, tab.gx, j, si), yr = lin(tab.s, tab.gy, j, si), psi = lin(tab.s, tab.gpsi, j, si);
     out[3 * (size_t)i] = xr - d[i] * sin(psi);
     out[3 * (size_t)i + 1] = yr + d[i] * cos(psi);
@@ -1975,7 +1988,9 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     if (device < 0 || device >= ndev) return fail(MPC_E_DEVICE, "device index out of range");
     HIPCHK(hipSetDevice(device), MPC_E_DEVICE);
     int tu = Tu < T ? Tu : T;   // limit = min(len(s), len(U))   trajectory_loader.py:73-75
-    std::vector<double> h((size_t)8 * T + 2 * tu);
+    // bucket index of the s column (seg_t): 4 buckets per table interval, ints after the doubles
+    const int nb = 4 * (T - 1);
+    std::vector<double> h((size_t)8 * T + 2 * tu + (nb + 2) / 2);
     double* s = h.data();
     for (int i = 0; i < T; ++i) {
         double si = X[5 * i];
@@ -2001,6 +2016,13 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         gpsi[i] = psi_new;
         gx[i] = gx[i - 1] + std::cos(psi_avg) * ds;
         gy[i] = gy[i - 1] + std::sin(psi_avg) * ds;
+    }
+    int* bidx = reinterpret_cast<int*>(h.data() + (size_t)8 * T + 2 * tu);
+    const double bh = (s[T - 1] - s[0]) / nb;
+    for (int g = 0, lo = 0; g <= nb; ++g) {
+        const double v = s[0] + g * bh;
+        while (lo < T && s[lo] < v) ++lo;
+        bidx[g] = lo;
     }
     mpc_ctx* c = (mpc_ctx*)std::calloc(1, sizeof(mpc_ctx));
     if (!c) return fail(MPC_E_ALLOC, "calloc");
@@ -2032,6 +2054,10 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     c->tab.T = T;
     c->tab.Tu = tu;
     c->tab.smax = s[T - 1];
+    c->tab.bidx = reinterpret_cast<const int*>(c->table_buf + (size_t)8 * T + 2 * tu);
+    c->tab.nb = nb;
+    c->tab.s0 = s[0];
+    c->tab.ibh = 1.0 / bh;
     for (int j = 0; j < 5; ++j) c->tab.last[j] = X[5 * (T - 1) + j];
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         hipFree(c->table_buf);
@@ -2112,6 +2138,7 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     if (split) {
         // the previous split launch may still be reading the list on another stream: order after it
         if (c->wl_pending && c->wl_stream != st) HIPCHK(hipStreamWaitEvent(st, c->wl_done, 0), MPC_E_DEVICE);
+        // reset by a memset on the stream (not by the kernels): a captured graph replays correctly
         HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
     }
     // obstacle rows exist only when obstacles are passed

@@ -64,6 +64,23 @@ def test_lookup_bit_exact(solvers, ti):
     assert np.array_equal(ct, g[f"t{ti}_control"])
 
 
+@pytest.mark.parametrize("ti", [1, 2, 3])
+def test_lookup_knots_vs_oracle(solvers, ti):
+    """The device interval search (bucket index + stepping) finds the binary search's interval at every
+    knot, one ulp either side of it, between knots, before s[0] and past s_max (oracle: bisection)."""
+    import oracle as O
+    X, U = traj_arrays(ti)
+    orc = O.Oracle(X, U)
+    knots = X[:, 0]
+    s = np.concatenate([knots, np.nextafter(knots, -np.inf), np.nextafter(knots, np.inf),
+                        0.5 * (knots[1:] + knots[:-1]), [-5.0, -1e-300, orc.s_max * 0.999999, orc.s_max + 3.0],
+                        np.random.default_rng(ti).uniform(-1.0, orc.s_max + 1.0, 2000)])
+    st, ct = solvers[ti].lookup(s)
+    for i, v in enumerate(s):
+        assert np.array_equal(st[i], orc.get_state(v)), (i, v)
+        assert np.array_equal(ct[i], orc.get_control(v)), (i, v)
+
+
 def test_warm_start_and_predict_bit_exact(lib, solvers):
     """sqp_iters=0 returns the warm start (:224-246) and predict(x0, ubar) (:87-114) unchanged."""
     cases, _ = golden_cases("warmstart_golden")
