@@ -980,6 +980,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     // the obstacle kernels hold 9 rows per lane, and there the looped solves need fewer registers
     // (fewer spills; measured C3 1.34 -> 1.24 ms)
     constexpr int NTR = OBS ? 0 : NT;
+    // row right-hand sides recomputed after the solve (WRC) instead of held live across it: obstacle
+    // kernels only (measured neutral on the obstacle-free N = 20 kernel)
+    constexpr bool WRC = OBS;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int ln = threadIdx.x;
     const int grp = ln / GL, gl = ln % GL;
@@ -1323,12 +1326,14 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int j = 0; j < NBOX; ++j) pbv[j] = 0.0;
             double sig = 0.0;
             bool breakdown = false;
-#ifdef MPC_PASS_UNROLL
+            // The passes (predictor, corrector, centred direction) are unrolled in the N = 20 kernels: no
+            // loop-carried copies of the predictor products at the back edge (C2 -3%).  The runtime-horizon
+            // kernels keep the loop (unrolled, C4 +2%, C5 +4%): their pass count is opaque, so the full-unroll
+            // request does not apply there (built with -Wno-pass-failed).
+            int npass = 3;
+            if constexpr (NT == 0) asm volatile("" : "+s"(npass));
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
-            for (int pass = 0; pass < 3; ++pass) {
+            for (int pass = 0; pass < npass; ++pass) {
                 // pass 0: affine predictor; 1: Mehrotra corrector; 2: plain centred direction, taken when
                 // the corrector would not reduce complementarity (oracle: comp_after > comp)
                 const double smu = (pass >= 1) ? sig * mu : 0.0;
@@ -1354,7 +1359,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
                     for (int j = 0; j < NR; ++j) {
                         double w;
-                        if constexpr (OBS) {
+                        if constexpr (WRC) {
                             w = row_wr(j);
                         } else {
                             const double r4 = fma(cw, p4v[j], fma(rs[j], rl[j], -smu));
@@ -1372,7 +1377,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
                     for (int j = 0; j < NBOX; ++j) {
                         double w;
-                        if constexpr (OBS) {
+                        if constexpr (WRC) {
                             w = box_wr(j);
                         } else {
                             const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
@@ -1412,7 +1417,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double r5 = fma(cw, p5v[j], fma(rxi[j], rnu[j], -smu));
                     const double rx = rho - rl[j] - rnu[j];
                     double wj;
-                    if constexpr (OBS) wj = row_wr(j); else wj = wr[j];
+                    if constexpr (WRC) wj = row_wr(j); else wj = wr[j];
                     const double dl = fma(-wv[j], rdot(rid<OBS>(j), cf[j], dx4), wj);
                     const double ds = -fma(rs[j], dl, r4) * il[j];
                     const double dn = rx - dl;
@@ -1431,7 +1436,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 for (int j = 0; j < NBOX; ++j) {
                     const double r4 = fma(cw, pbv[j], fma(sb[j], lb[j], -smu));
                     double wj;
-                    if constexpr (OBS) wj = box_wr(j); else wj = wrb[j];
+                    if constexpr (WRC) wj = box_wr(j); else wj = wrb[j];
                     const double dl = fma(-wb[j] * bsign(j), (j < 2 ? dd0 : dd1), wj);
                     const double ds = -fma(sb[j], dl, r4) * ilb[j];
                     dsb[j] = ds;
