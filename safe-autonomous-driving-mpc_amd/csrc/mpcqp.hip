@@ -175,6 +175,12 @@ struct Lds {
 // the forward solve reads closed-loop rows (AC) in the horizon-specialised kernels and for GL = 64; the
 // runtime-horizon GL <= 32 kernels keep the K-row form (AC would cost them an occupancy step at N ~ 30)
 __host__ __device__ constexpr bool acl_on(int GL, int NT) { return NT > 0 || GL == 64; }
+// The crossover launch (MODE_XO) carves a lite layout: no AC (K-row forward solve), no cost data (held
+// in registers: lane k-1 is its only writer and reader), no dual-residual terms (ys, zs; interior point
+// only), and the direction dud aliases gh (gh is dead once kk is formed; dud is read only after the
+// solve, and every solve's caller rewrites gh first).  At N = 20 that is 1251 doubles per instance, so
+// 8 two-instance workgroups (20 KB each) fit the 160 KB of a CU: all 2048 crossover waves of a 4096
+// batch are resident at once, two per SIMD, instead of running in two rounds.
 // At convergence the separate dual-residual terms (yc, ya, zc, za) go to a scratch in QR rows 0..2
 // (the factorisation is dead then; the polish rewrites those rows): yc of stage k at QR[k][0..3],
 // ya at QR[k][4..7], zc / za of control t at QR[t][8..9] / QR[t][10..11].
@@ -183,20 +189,20 @@ __host__ __device__ constexpr bool acl_on(int GL, int NT) { return NT > 0 || GL 
 #define DQ_ZC 8
 #define DQ_ZA 10
 
-__host__ __device__ inline int lds_doubles(int N, bool acl) {
+__host__ __device__ inline int lds_doubles(int N, bool acl, bool lite = false) {
     int NP = N + 1;
-    int n = (acl ? N * 30 : 0) + N * A5S + NP * 6 + NP * QRS + N * 2 + N * KRS + N * SIS + NP * QHS + N * 2 + N * 2 + NP * 4 +
-            N * 2 + N * 2 + NP * 5;
+    int n = (acl ? N * 30 : 0) + N * A5S + (lite ? 0 : NP * 6) + NP * QRS + N * 2 + N * KRS + N * SIS + NP * QHS + N * 2 +
+            (lite ? 0 : N * 2 + NP * 4 + N * 2) + N * 2 + NP * 5;
     return (n + 1) & ~1;     // groups stay 16-B aligned
 }
 
-__device__ inline Lds carve(double* p, int N, bool acl) {
+__device__ inline Lds carve(double* p, int N, bool acl, bool lite = false) {
     Lds L;
     int NP = N + 1;
     // even-sized arrays first (16-B aligned starts), the odd-sized ones last
     L.AC = p; p += acl ? N * 30 : 0;
     L.A5 = p; p += N * A5S;
-    L.cst = p; p += NP * 6;
+    L.cst = lite ? nullptr : p; p += lite ? 0 : NP * 6;
     L.QR = p; p += NP * QRS;
     L.Rt = p; p += N * 2;
     L.KR = p; p += N * KRS;
@@ -206,9 +212,9 @@ __device__ inline Lds carve(double* p, int N, bool acl) {
     L.kap = p + NP * 5;
     p += NP * QHS;
     L.gh = p; p += N * 2;
-    L.dud = p; p += N * 2;
-    L.ys = p; p += NP * 4;
-    L.zs = p; p += N * 2;
+    L.dud = lite ? L.gh : p; p += lite ? 0 : N * 2;
+    L.ys = lite ? nullptr : p; p += lite ? 0 : NP * 4;
+    L.zs = lite ? nullptr : p; p += lite ? 0 : N * 2;
     L.ub = p; p += N * 2;
     L.dX = p; p += NP * 5;
     return L;
@@ -290,11 +296,28 @@ __device__ __forceinline__ double dpp_d(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
-__device__ __forceinline__ double swz16_d(double v) {          // lane ^ 16 within each 32-lane half
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_swizzle((int)(unsigned)b, 0x401F);
-    const int hi = __builtin_amdgcn_ds_swizzle((int)(unsigned)(b >> 32), 0x401F);
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+// Row pairs and wave halves: v_permlane16_swap / v_permlane32_swap with the value in both operands
+// return both sides of the pair (rows 2r and 2r+1 of 16 lanes; lanes i and i+32) on every lane, in two
+// VALU slots per double and no LDS round trip (ds_swizzle / ds_bpermute wait ~60-80 cycles per hop).
+// tools/probes/xlane_probe.hip checks the semantics.
+__device__ __forceinline__ double pack_d(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int W>
+__device__ __forceinline__ void xpair_d(double v, double& a, double& b) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    if constexpr (W == 16) {
+        const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        a = pack_d(l[0], h[0]);
+        b = pack_d(l[1], h[1]);
+    } else {
+        const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        a = pack_d(l[0], h[0]);
+        b = pack_d(l[1], h[1]);
+    }
 }
 #define DPP_XOR1 0xB1          // quad_perm [1,0,3,2]
 #define DPP_XOR2 0x4E          // quad_perm [2,3,0,1]
@@ -310,8 +333,10 @@ struct Grp {
         v = op(v, dpp_d<DPP_XOR2>(v));
         v = op(v, dpp_d<DPP_HMIRROR>(v));
         v = op(v, dpp_d<DPP_MIRROR>(v));
-        if (GL >= 32) v = op(v, swz16_d(v));
-        if (GL >= 64) v = op(v, __shfl_xor(v, 32, WAVE));
+        // the same (a, b) operand order on both sides of a pair: every lane ends bit-identical
+        double a, b;
+        if (GL >= 32) { xpair_d<16>(v, a, b); v = op(a, b); }
+        if (GL >= 64) { xpair_d<32>(v, a, b); v = op(a, b); }
         return v;
     }
     __device__ __forceinline__ double sum(double v) const {
@@ -969,7 +994,7 @@ __device__ __forceinline__ constexpr int rid(int j) { return OBS ? j : (j < 6 ? 
 
 // NT > 0: kernel specialised for horizon N = NT (the stage recursions are unrolled); NT = 0: any N.
 template <int GL, bool OBS, int MODE, int NT>
-__global__ void __launch_bounds__(WAVE)
+__global__ void __launch_bounds__(WAVE, MODE == MODE_XO ? 2 : 1)   // crossover: two waves per SIMD (256 VGPRs)
 mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g, const double* __restrict__ obsg,
                  const int* __restrict__ nobsg, const double* __restrict__ ubarg, double* __restrict__ u0g,
                  double* __restrict__ Ug, double* __restrict__ Xg, int* __restrict__ statusg,
@@ -1007,8 +1032,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     const double dt = Pr.dt;
     const double rho = Pr.rho;
     const double hL = Pr.L / 2.0;
-    constexpr bool ACL = acl_on(GL, NT);
-    Lds S = carve(smem + (size_t)grp * lds_doubles(N, ACL), N, ACL);
+    constexpr bool LITE = MODE == MODE_XO;          // lite LDS layout (see lds_doubles)
+    constexpr bool ACL = acl_on(GL, NT) && !LITE;
+    Lds S = carve(smem + (size_t)grp * lds_doubles(N, ACL, LITE), N, ACL, LITE);
 
     double x0[5];
 #pragma unroll
@@ -1064,7 +1090,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 
     const int nsqp = Pr.sqp_iters < 0 ? 0 : Pr.sqp_iters;   // 0: return ubar and predict(x0, ubar)
     int status = MPC_OK, total_it = 0;
-    bool xo_ok = false;              // MODE_XO: the crossover certified this instance
+    bool xo_ok = false;
+    double cstr[6] = {0, 0, 0, 0, 0, 0};   // LITE: cost data of stage k (this lane's only)              // MODE_XO: the crossover certified this instance
     for (int sqp = 0; sqp < nsqp; ++sqp) {
         // ---- K1: nominal rollout == predict(x0, ubar), into Xr ------------------------------
         predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
@@ -1106,12 +1133,13 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             const double sk0 = Q.get(slk[0], src), sk1 = Q.get(slk[1], src), sk3 = Q.get(slk[3], src);
             if (live) {
                 const double* x = S.Xr + 5 * k;
-                S.cst[6 * k + 0] = gn ? -sk0 : 0.0;
-                S.cst[6 * k + 1] = gn ? -sk1 : 0.0;
-                S.cst[6 * k + 2] = gn ? -sk3 : 0.0;
-                S.cst[6 * k + 3] = x[1] - rk1;
-                S.cst[6 * k + 4] = x[2] - rk2;
-                S.cst[6 * k + 5] = x[4] - rk4;
+                double* c = LITE ? cstr : S.cst + 6 * k;
+                c[0] = gn ? -sk0 : 0.0;
+                c[1] = gn ? -sk1 : 0.0;
+                c[2] = gn ? -sk3 : 0.0;
+                c[3] = x[1] - rk1;
+                c[4] = x[2] - rk2;
+                c[5] = x[4] - rk4;
             }
         }
         // row bounds of stage k, box bounds of control k-1
@@ -1223,7 +1251,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             // multipliers); ya (row multipliers) accumulated above
             auto dual_terms = [&](double yc[4], double zc[2], double za[2]) {
                 double Qs[10], qs[4];
-                stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
+                stage_cost(LITE ? cstr : S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
                 for (int a = 0; a < 4; ++a) {
                     double acc = qs[a];
@@ -1305,7 +1333,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 }
                 if (live) {
                     double Qs[10], qs[4];
-                    stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
+                    stage_cost(LITE ? cstr : S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -1554,7 +1582,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                                     Qp[p4(a, c)] = fma(w * cf[j][a], cf[j][c], Qp[p4(a, c)]);
                     }
                     double Qs[10], qs[4];
-                    stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
+                    stage_cost(LITE ? cstr : S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
                     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -1590,7 +1618,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                             if (j < 2) g0 += v; else g1 += v;
                         }
                         double Qs[10], qs[4];
-                        stage_cost(S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
+                        stage_cost(LITE ? cstr : S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
                         for (int a = 0; a < 4; ++a) {
                             double acc = qs[a];
@@ -1604,7 +1632,12 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         S.gh[2 * (k - 1) + 1] = g1 - fma(R1, pu1, R1 * S.ub[2 * (k - 1) + 1]);
                     }
                     wave_sync();
-                    riccati_solve<NTR, ACL>(S, N, dt, gl);
+                    // the crossover (phase 0) solves in K-row form wherever the two-phase launch exists
+                    // (G >= 2): the MODE_XO launch has no AC rows (lite LDS layout), and MODE_FULL must give
+                    // bit-identical results.  GL = 64 (G = 1) is never split and keeps the AC rows (the
+                    // K-row crossover cost C5 4%).
+                    if (ACL && (phase == 1 || GL == 64)) riccati_solve<NTR, ACL>(S, N, dt, gl);
+                    else riccati_solve<NTR, false>(S, N, dt, gl);
                     {
                         double dx4[4];
 #pragma unroll
@@ -2130,6 +2163,7 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     const bool nt20 = kp.N == 20 && !MPC_NO_NT20;
     const size_t lds_wave = sizeof(double) * (size_t)lds_doubles(kp.N, acl_on(GL, nt20 ? 20 : 0)) * G;
     if (lds_wave > 160 * 1024) return fail(MPC_E_ARG, "horizon too long for LDS");
+    const size_t lds_lite = sizeof(double) * (size_t)lds_doubles(kp.N, false, true) * G;   // MODE_XO
     const dim3 grid((B + G - 1) / G);
     // Two-phase launch (MODE_XO then MODE_IPM) for single-QP solves with the crossover on; the work
     // list lives in the context (one list per context: a context is not re-entrant, include/mpcqp.h).
@@ -2148,7 +2182,8 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     }
     // obstacle rows exist only when obstacles are passed
 #define MPC_LAUNCH(GLV, OBSV, MODEV, NTV)                                                                   \
-    hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV, MODEV, NTV>), grid, dim3(WAVE), lds_wave, st, c->tab, kp, B, \
+    hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV, MODEV, NTV>), grid, dim3(WAVE),                    \
+                       MODEV == MODE_XO ? lds_lite : lds_wave, st, c->tab, kp, B,                           \
                        x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt)
     // horizon-specialised kernels for the BASELINE horizons that pay for their code size (N = 20)
 #define MPC_LAUNCH_GL(MODEV)                                                                   \
