@@ -282,6 +282,27 @@ __device__ __forceinline__ double frcp(double x) {
     return fma(r, e, r);
 }
 
+// v_max_f64 / v_min_f64 as single instructions.  For fmax/fmin LLVM first quiets every operand it
+// cannot prove canonical (DPP and permlane results, selects, loop-carried values) with an extra
+// v_max_f64 x, x, x; arithmetic here only ever makes quiet NaNs, for which the bare instruction already
+// has fmax's semantics (the other operand wins), so results are unchanged.
+__device__ __forceinline__ double vmax(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmin(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// max(a, |b|)
+__device__ __forceinline__ double vmaxabs(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // ------------------------------------------------------------------------------------------
 // lane groups: IPW instances per 64-lane wavefront, GL = 64 / IPW lanes each
 // ------------------------------------------------------------------------------------------
@@ -343,10 +364,10 @@ struct Grp {
         return reduce(v, [](double a, double b) { return a + b; });
     }
     __device__ __forceinline__ double max(double v) const {
-        return reduce(v, [](double a, double b) { return fmax(a, b); });
+        return reduce(v, [](double a, double b) { return vmax(a, b); });
     }
     __device__ __forceinline__ double min(double v) const {
-        return reduce(v, [](double a, double b) { return fmin(a, b); });
+        return reduce(v, [](double a, double b) { return vmin(a, b); });
     }
     __device__ __forceinline__ double get(double v, int rel) const { return __shfl(v, base + rel, WAVE); }
 };
@@ -1243,8 +1264,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 const double rx = rho - rl[j] - rnu[j];
 #pragma unroll
                 for (int a = 0; a < 4; ++a) ya[a] = fma(-rl[j], cf[j][a], ya[a]);
-                rpmax = fmax(rpmax, fabs(rp));
-                rxmax = fmax(rxmax, fabs(rx));
+                rpmax = vmaxabs(rpmax, rp);
+                rxmax = vmaxabs(rxmax, rx);
                 comp = fma(rs[j], rl[j], fma(rxi[j], rnu[j], comp));
             }
             // dual-residual stage terms of stage k / control k-1: yc (cost), zc (control cost), za (box
@@ -1268,7 +1289,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j) {
                     const double rp = bsign(j) * (j < 2 ? du0 : du1) - sb[j] - bb[j];
-                    rpmax = fmax(rpmax, fabs(rp));
+                    rpmax = vmaxabs(rpmax, rp);
                     comp = fma(sb[j], lb[j], comp);
                 }
                 double yc[4], zc[2], za[2];
@@ -1455,10 +1476,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     dlv[j] = on ? dl : 0.0;
                     dxv[j] = on ? dxi : 0.0;
                     dnv[j] = on ? dn : 0.0;
-                    rmax = fmax(rmax, -dsv[j] * __builtin_amdgcn_rcp(rs[j]));
-                    rmax = fmax(rmax, -dlv[j] * il[j]);
-                    rmax = fmax(rmax, -dxv[j] * __builtin_amdgcn_rcp(rxi[j]));
-                    rmax = fmax(rmax, -dnv[j] * inu[j]);
+                    rmax = vmax(rmax, -dsv[j] * __builtin_amdgcn_rcp(rs[j]));
+                    rmax = vmax(rmax, -dlv[j] * il[j]);
+                    rmax = vmax(rmax, -dxv[j] * __builtin_amdgcn_rcp(rxi[j]));
+                    rmax = vmax(rmax, -dnv[j] * inu[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j) {
@@ -1469,8 +1490,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     const double ds = -fma(sb[j], dl, r4) * ilb[j];
                     dsb[j] = ds;
                     dlb[j] = dl;
-                    rmax = fmax(rmax, -dsb[j] * __builtin_amdgcn_rcp(sb[j]));
-                    rmax = fmax(rmax, -dlb[j] * ilb[j]);
+                    rmax = vmax(rmax, -dsb[j] * __builtin_amdgcn_rcp(sb[j]));
+                    rmax = vmax(rmax, -dlb[j] * ilb[j]);
                 }
                 const double amax = __builtin_amdgcn_rcp(Q.max(live ? rmax : 1.0));
                 // complementarity after the step (pass 0: at the full affine step length)
@@ -1660,10 +1681,10 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 double lmax = 1.0;
 #pragma unroll
                 for (int j = 0; j < NR; ++j)
-                    if (cls[j] == 1) lmax = fmax(lmax, fabs(tl[j]));
+                    if (cls[j] == 1) lmax = vmaxabs(lmax, tl[j]);
 #pragma unroll
                 for (int j = 0; j < NBOX; ++j)
-                    if (clb[j] == 1) lmax = fmax(lmax, fabs(tlb[j]));
+                    if (clb[j] == 1) lmax = vmaxabs(lmax, tlb[j]);
                 lmax = Q.max(lmax);
                 // a row is offending when its KKT condition fails (oracle polish_from: bad > 0); only the
                 // flags matter, so no division by the scales (each IEEE division is ~10 instructions)
