@@ -61,18 +61,22 @@ def main():
     import torch
     import torch.distributed as dist
     import __graft_entry__ as ge
-    ge.build()
-    import mpcqp
-    import workloads as W
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one build per node (a no-op when the in-tree libraries are current); the other ranks load them
+    # after the barrier below
+    if local == 0:
+        ge.build()
+    import mpcqp
+    import workloads as W
+
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (libmpcqp has no CPU backend)")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
+        dist.barrier()
     dev = torch.device("cuda", local)
 
     import shard
