@@ -264,22 +264,37 @@ __device__ __forceinline__ double rdot(int j, const double c[4], const double x[
         }
     return acc;
 }
-// 1/sqrt(x) to full double precision: v_rsq_f64 + two Newton steps (the Cholesky pivots only
+// 1/sqrt(x) to full double precision: v_rsq_f64 + one third-order correction (the Cholesky pivots only
 // enter as reciprocals; the IEEE sqrt sequence costs ~100 cycles of dependent latency on gfx950)
+#ifndef MPC_HO_RECIP
+#define MPC_HO_RECIP 1
+#endif
 __device__ __forceinline__ double frsqrt(double x) {
     double y = __builtin_amdgcn_rsq(x);
+#if MPC_HO_RECIP
+    // one third-order step: with e = 1 - x y^2 (|e| < 2^-22 from v_rsq_f64), 1/sqrt(x) =
+    // y (1 + e/2 + 3e^2/8 + O(e^3)); 4 dependent levels instead of the 6 of two Newton steps
+    const double e = fma(-x * y, y, 1.0);
+    return fma(y * e, fma(0.375, e, 0.5), y);
+#else
     const double h = 0.5 * x;
     y = y * fma(-h * y, y, 1.5);
     y = y * fma(-h * y, y, 1.5);
     return y;
+#endif
 }
-// 1/x to full double precision: v_rcp_f64 + two Newton steps (no IEEE division sequence)
+// 1/x to full double precision: v_rcp_f64 + one third-order correction (no IEEE division sequence)
 __device__ __forceinline__ double frcp(double x) {
     double r = __builtin_amdgcn_rcp(x);
     double e = fma(-x, r, 1.0);
+#if MPC_HO_RECIP
+    // one third-order step: 1/x = r (1 + e + e^2 + O(e^3)) with e = 1 - x r
+    return fma(r, fma(e, e, e), r);
+#else
     r = fma(r, e, r);
     e = fma(-x, r, 1.0);
     return fma(r, e, r);
+#endif
 }
 
 // v_max_f64 / v_min_f64 as single instructions.  For fmax/fmin LLVM first quiets every operand it
