@@ -65,12 +65,16 @@ def assert_identical(a, b, what):
         assert np.array_equal(a[k], b[k]), (what, k, np.flatnonzero((a[k] != b[k]).reshape(len(a[k]), -1).any(1))[:8])
 
 
-@pytest.mark.parametrize("cfg,B", [("C2", 1024), ("C3", 1024)])
-def test_two_phase_equals_single_kernel(lib, cfg, B):
-    """Split launch (MODE_XO + MODE_IPM) == single launch (MODE_FULL), host and device entries."""
+@pytest.mark.parametrize("cfg,B,N", [("C2", 1024, None), ("C3", 1024, None), ("C4", 1024, None), ("C2", 1024, 10)])
+def test_two_phase_equals_single_kernel(lib, cfg, B, N):
+    """Split launch (MODE_XO + MODE_IPM) == single launch (MODE_FULL), host and device entries.  Covers the
+    N = 20 kernels (C2, C3), the runtime-horizon GL = 32 kernels (C4, N = 30) and GL = 16 (N = 10, four
+    instances per wavefront); the crossover solves in K-row form in both launch paths."""
     torch = pytest.importorskip("torch")
     import workloads as W
     wb = W.make_batch(cfg, B=B, seed=7)
+    if N is not None:
+        wb["N"] = N
     two = make_solver(lib, wb["traj"], wb["N"], wb["max_obs"], two_phase=True)
     one = make_solver(lib, wb["traj"], wb["N"], wb["max_obs"], two_phase=False)
     r2 = two.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
