@@ -60,7 +60,9 @@ typedef struct mpc_params {
     double brake_accel;             /* warm start braking control u2 (:240, -2.0)                    */
     /* solver */
     int linearization;              /* 1 = Gauss-Newton (reference slopes, default), 0 = frozen refs  */
-    int sqp_iters;                  /* QP solves per call: 1 = single QP at ubar (parity gate);
+    int sqp_iters;                  /* QP solves per call (at most, see sqp_tol): 1 = single QP at ubar
+                                       (the tracking-QP parity gate); > 1 = Gauss-Newton SQP on the
+                                       reference's nonlinear problem, re-linearised about each solution;
                                        0 = no solve: U = ubar, Xpred = predict(x0, ubar)              */
     int max_iter;                   /* PDIP iteration cap per QP                                     */
     int polish;                     /* 0 off; 1 active-set polish of the interior-point result;
@@ -69,6 +71,8 @@ typedef struct mpc_params {
     double tol;                     /* relative primal/dual residual tolerance                        */
     double tol_mu;                  /* absolute complementarity tolerance                             */
     double elastic_rho;             /* L1 penalty of the elastic (soft) state rows                    */
+    double sqp_tol;                 /* SQP stops early once a re-linearised QP moves U by at most this
+                                       (max-norm); 0 = always run sqp_iters QPs                        */
 } mpc_params;
 
 typedef struct mpc_ctx mpc_ctx;

@@ -65,6 +65,7 @@ void orc_default_params(mpc_params* p) {
     p->tol_mu = 1e-9;
     p->elastic_rho = 1e5;
     p->polish = 2;
+    p->sqp_tol = 1e-10;
 }
 
 static int seg(const double* x, int n, double v);
@@ -1105,8 +1106,13 @@ int orc_solve(const orc_table* t, const mpc_params* p, const double x0[5], const
         int ni = 0;
         status = pdip(&Q, p, &S, &ni);
         total += ni;
-        for (int i = 0; i < 2 * N; ++i) Uo[i] = ub[i] + S.du[i];
+        double step = 0.0;
+        for (int i = 0; i < 2 * N; ++i) {
+            Uo[i] = ub[i] + S.du[i];
+            step = fabs(S.du[i]) > step ? fabs(S.du[i]) : step;
+        }
         memcpy(ub, Uo, sizeof(double) * 2 * N);
+        if (nsqp > 1 && step <= p->sqp_tol) break;   /* converged re-linearisation */
     }
     if (U) memcpy(U, Uo, sizeof(double) * 2 * N);
     if (u0) { u0[0] = Uo[0]; u0[1] = Uo[1]; }

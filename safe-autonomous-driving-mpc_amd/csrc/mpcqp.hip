@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/mpcqp.h"
+#include "host_table.h"
 
 #define WAVE 64
 #ifndef MPC_NO_NT20
@@ -62,7 +63,7 @@ struct KParams {
     double dt, u_min0, u_min1, u_max0, u_max1;
     double w_d, w_o, w_v, w_u1, w_u2;
     double osd, tgap, L, sl, brake_distance, brake_accel;
-    double tol, tol_mu, rho;
+    double tol, tol_mu, rho, sqp_tol;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -89,16 +90,22 @@ __device__ __forceinline__ void wave_sync() { __syncthreads(); }
 // reference signal: scipy interp1d 'linear' + extrapolate (scipy _interpolate.py:457-483)
 // ------------------------------------------------------------------------------------------
 // interval of v in the table's s column (n <= T: a prefix of it), i.e. scipy's searchsorted
-// (lower bound) clamped to [1, n - 1].  The lower bound is found from the bucket index (one load) and
-// corrected by stepping, so the result is the binary search's exactly while the dependent chain is
-// ~2 L2 loads instead of log2(T) (every instance looks up ~4 N times)
+// (lower bound) clamped to [1, n - 1].  v's bucket g brackets the lower bound: it lies in
+// [bidx[g - 1], bidx[g + 2]] (one bucket of slack either side for the rounding of g), so a binary search
+// over that window returns the full binary search's answer exactly.  With 4 buckets per table interval
+// the window holds ~1 knot (~2 dependent L2 loads instead of log2 T; every instance looks up ~4 N times),
+// and a table with clustered knots costs log2 of the knots in the window, never a linear walk.
+// Host restatement: mpcqp_host::seg_host (host_table.h).
 __device__ __forceinline__ int seg_t(const DevTable& t, int n, double v) {
     double gf = (v - t.s0) * t.ibh;
     gf = gf > 0.0 ? gf : 0.0;                       // also maps NaN to bucket 0
     const int g = gf < (double)(t.nb - 1) ? (int)gf : t.nb - 1;
-    int lo = t.bidx[g];
-    while (lo < t.T && t.s[lo] < v) ++lo;
-    while (lo > 0 && !(t.s[lo - 1] < v)) --lo;
+    int lo = t.bidx[g > 0 ? g - 1 : 0];
+    int hi = g + 2 <= t.nb ? t.bidx[g + 2] : t.T;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (t.s[mid] < v) lo = mid + 1; else hi = mid;
+    }
     lo = lo < n ? lo : n;
     lo = lo < 1 ? 1 : lo;
     lo = lo > n - 1 ? n - 1 : lo;
@@ -1767,6 +1774,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             S.ub[2 * (k - 1) + 1] += du1;
         }
         wave_sync();
+        // SQP: stop once the re-linearised QP no longer moves U (oracle orc_solve; group-uniform)
+        if (nsqp > 1 && Q.max(live ? vmaxabs(fabs(du0), du1) : 0.0) <= Pr.sqp_tol) break;
     }
 
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------
@@ -1997,6 +2006,7 @@ extern "C" void mpc_default_params(mpc_params* p) {
     p->tol_mu = 1e-9;
     p->elastic_rho = 1e5;
     p->polish = 2;
+    p->sqp_tol = 1e-10;
 }
 
 extern "C" const char* mpc_last_error(void) { return g_err.c_str(); }
@@ -2022,6 +2032,7 @@ static int check_params(const mpc_params* p) {
     if (p->max_iter < 1) return fail(MPC_E_ARG, "max_iter must be >= 1");
     if (p->sqp_iters < 0 || p->sqp_iters > 100) return fail(MPC_E_ARG, "sqp_iters out of range [0, 100]");
     if (!(p->elastic_rho > 1.0)) return fail(MPC_E_ARG, "elastic_rho must be > 1");
+    if (!(p->sqp_tol >= 0.0)) return fail(MPC_E_ARG, "sqp_tol must be >= 0");
     return MPC_SUCCESS;
 }
 
@@ -2046,6 +2057,7 @@ static KParams kparams(const mpc_params* p) {
     k.tol_mu = p->tol_mu;
     k.rho = p->elastic_rho;
     k.polish = p->polish;
+    k.sqp_tol = p->sqp_tol;
     return k;
 }
 
@@ -2061,43 +2073,10 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         return fail(MPC_E_DEVICE, "no HIP device available (libmpcqp has no CPU backend)");
     if (device < 0 || device >= ndev) return fail(MPC_E_DEVICE, "device index out of range");
     HIPCHK(hipSetDevice(device), MPC_E_DEVICE);
-    int tu = Tu < T ? Tu : T;   // limit = min(len(s), len(U))   trajectory_loader.py:73-75
-    // bucket index of the s column (seg_t): 4 buckets per table interval, ints after the doubles
-    const int nb = 4 * (T - 1);
-    std::vector<double> h((size_t)8 * T + 2 * tu + (nb + 2) / 2);
-    double* s = h.data();
-    for (int i = 0; i < T; ++i) {
-        double si = X[5 * i];
-        if (i > 0 && si <= s[i - 1]) si = s[i - 1] + 1e-5;   // trajectory_loader.py:28-30
-        s[i] = si;
-        h[T + i] = X[5 * i + 1];
-        h[2 * T + i] = X[5 * i + 2];
-        h[3 * T + i] = X[5 * i + 3];
-        h[4 * T + i] = X[5 * i + 4];
-    }
-    for (int i = 0; i < tu; ++i) { h[5 * T + i] = U[2 * i]; h[5 * T + tu + i] = U[2 * i + 1]; }
-    // global pose of the reference line: heading integrates X[i-1,3] over ds, position the mean
-    // heading of each step (trajectory_loader.py:38-58; host libm, as numpy)
-    double* gx = h.data() + 5 * T + 2 * tu;
-    double* gy = gx + T;
-    double* gpsi = gy + T;
-    gx[0] = gy[0] = gpsi[0] = 0.0;
-    for (int i = 1; i < T; ++i) {
-        const double ds = s[i] - s[i - 1];
-        const double psi_old = gpsi[i - 1];
-        const double psi_new = psi_old + X[5 * (i - 1) + 3] * ds;
-        const double psi_avg = (psi_old + psi_new) / 2.0;
-        gpsi[i] = psi_new;
-        gx[i] = gx[i - 1] + std::cos(psi_avg) * ds;
-        gy[i] = gy[i - 1] + std::sin(psi_avg) * ds;
-    }
-    int* bidx = reinterpret_cast<int*>(h.data() + (size_t)8 * T + 2 * tu);
-    const double bh = (s[T - 1] - s[0]) / nb;
-    for (int g = 0, lo = 0; g <= nb; ++g) {
-        const double v = s[0] + g * bh;
-        while (lo < T && s[lo] < v) ++lo;
-        bidx[g] = lo;
-    }
+    mpcqp_host::HostTable ht;      // monotone s fix, interp columns, global line, bucket index (host_table.h)
+    if (!mpcqp_host::build_host_table(X, T, U, Tu, ht)) return fail(MPC_E_ARG, "bad trajectory table");
+    const std::vector<double>& h = ht.buf;
+    const int tu = ht.tu;
     mpc_ctx* c = (mpc_ctx*)std::calloc(1, sizeof(mpc_ctx));
     if (!c) return fail(MPC_E_ALLOC, "calloc");
     c->device = device;
@@ -2127,12 +2106,12 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     c->tab.gpsi = c->tab.gy + T;
     c->tab.T = T;
     c->tab.Tu = tu;
-    c->tab.smax = s[T - 1];
-    c->tab.bidx = reinterpret_cast<const int*>(c->table_buf + (size_t)8 * T + 2 * tu);
-    c->tab.nb = nb;
-    c->tab.s0 = s[0];
-    c->tab.ibh = 1.0 / bh;
-    for (int j = 0; j < 5; ++j) c->tab.last[j] = X[5 * (T - 1) + j];
+    c->tab.smax = ht.smax;
+    c->tab.bidx = reinterpret_cast<const int*>(c->table_buf + ht.off_bidx);
+    c->tab.nb = ht.nb;
+    c->tab.s0 = ht.s0;
+    c->tab.ibh = ht.ibh;
+    for (int j = 0; j < 5; ++j) c->tab.last[j] = ht.last[j];
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         hipFree(c->table_buf);
         std::free(c);
@@ -2468,96 +2447,6 @@ extern "C" int mpc_global_pose(mpc_ctx* c, int n, const double* s, const double*
     return rc;
 }
 
-// ------------------------------------------------------------------------------------------
-// trajectory JSON (the reference's format: {"X": [[s,d,o,k,v], ...], "U": [[u1,u2], ...], ...},
-// trajectory_loader.py:13-24); a small recursive-descent reader, host only
-// ------------------------------------------------------------------------------------------
-namespace {
-struct JsonReader {
-    const char* p;
-    const char* end;
-    std::string err;
-    void ws() { while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p; }
-    bool expect(char ch) {
-        ws();
-        if (p < end && *p == ch) { ++p; return true; }
-        err = std::string("expected '") + ch + "'";
-        return false;
-    }
-    bool string(std::string* out) {
-        if (!expect('"')) return false;
-        std::string r;
-        while (p < end && *p != '"') {
-            if (*p == '\\' && p + 1 < end) { r.push_back(p[1]); p += 2; }
-            else r.push_back(*p++);
-        }
-        if (p >= end) { err = "unterminated string"; return false; }
-        ++p;
-        if (out) *out = r;
-        return true;
-    }
-    bool number(double* out) {
-        ws();
-        char* e = nullptr;
-        double v = std::strtod(p, &e);
-        if (e == p) { err = "expected a number"; return false; }
-        p = e;
-        *out = v;
-        return true;
-    }
-    bool skip() {   // any value
-        ws();
-        if (p >= end) { err = "unexpected end"; return false; }
-        if (*p == '"') return string(nullptr);
-        if (*p == '{' || *p == '[') {
-            const char open = *p, close = open == '{' ? '}' : ']';
-            ++p;
-            ws();
-            if (p < end && *p == close) { ++p; return true; }
-            while (true) {
-                if (open == '{') { if (!string(nullptr) || !expect(':')) return false; }
-                if (!skip()) return false;
-                ws();
-                if (p < end && *p == ',') { ++p; continue; }
-                return expect(close);
-            }
-        }
-        if (!std::strncmp(p, "true", 4)) { p += 4; return true; }
-        if (!std::strncmp(p, "false", 5)) { p += 5; return true; }
-        if (!std::strncmp(p, "null", 4)) { p += 4; return true; }
-        double v;
-        return number(&v);
-    }
-    // [[a, b, ...], ...] with rows of exactly `width` numbers
-    bool matrix(int width, std::vector<double>* out, int* rows) {
-        if (!expect('[')) return false;
-        *rows = 0;
-        ws();
-        if (p < end && *p == ']') { ++p; return true; }
-        while (true) {
-            if (!expect('[')) return false;
-            for (int j = 0; j < width; ++j) {
-                double v;
-                if (!number(&v)) return false;
-                out->push_back(v);
-                if (j + 1 < width && !expect(',')) {
-                    err = "row of the wrong width (expected " + std::to_string(width) + " numbers)";
-                    return false;
-                }
-            }
-            if (!expect(']')) {
-                err = "row of the wrong width (expected " + std::to_string(width) + " numbers)";
-                return false;
-            }
-            ++*rows;
-            ws();
-            if (p < end && *p == ',') { ++p; continue; }
-            return expect(']');
-        }
-    }
-};
-}  // namespace
-
 extern "C" int mpc_read_trajectory_json(const char* path, double* X, int maxT, double* U, int maxTu, int* T,
                                         int* Tu) {
     if (!path || !T || !Tu) return fail(MPC_E_ARG, "path, T and Tu are required");
@@ -2568,37 +2457,20 @@ extern "C" int mpc_read_trajectory_json(const char* path, double* X, int maxT, d
     size_t got;
     while ((got = std::fread(chunk, 1, sizeof(chunk), f)) > 0) text.append(chunk, got);
     std::fclose(f);
-    JsonReader r{text.data(), text.data() + text.size(), ""};
+    // host_table.h: json.load semantics (last duplicate key wins, bounded nesting, no trailing data)
     std::vector<double> xs, us;
-    int tx = -1, tu = -1;
-    bool ok = r.expect('{');
-    r.ws();
-    if (ok && r.p < r.end && *r.p == '}') ok = false, r.err = "empty object";
-    while (ok) {
-        std::string key;
-        ok = r.string(&key) && r.expect(':');
-        if (!ok) break;
-        if (key == "X") ok = r.matrix(5, &xs, &tx);
-        else if (key == "U") ok = r.matrix(2, &us, &tu);
-        else ok = r.skip();
-        if (!ok) break;
-        r.ws();
-        if (r.p < r.end && *r.p == ',') { ++r.p; continue; }
-        ok = r.expect('}');
-        break;
-    }
-    if (!ok) return fail(MPC_E_ARG, std::string("trajectory JSON: ") + r.err + " at byte " +
-                                        std::to_string((long)(r.p - text.data())));
-    if (tx < 0 || tu < 0) return fail(MPC_E_ARG, "trajectory JSON: missing 'X' or 'U'");
+    int tx = 0, tu = 0;
+    std::string err;
+    if (!mpcqp_host::read_trajectory_json_text(text, xs, tx, us, tu, err)) return fail(MPC_E_ARG, err);
     *T = tx;
     *Tu = tu;
     if (X) {
         if (maxT < tx) return fail(MPC_E_ARG, "X buffer too small");
-        std::memcpy(X, xs.data(), sizeof(double) * xs.size());
+        std::memcpy(X, xs.data(), sizeof(double) * 5 * (size_t)tx);
     }
     if (U) {
         if (maxTu < tu) return fail(MPC_E_ARG, "U buffer too small");
-        std::memcpy(U, us.data(), sizeof(double) * us.size());
+        std::memcpy(U, us.data(), sizeof(double) * 2 * (size_t)tu);
     }
     return MPC_SUCCESS;
 }

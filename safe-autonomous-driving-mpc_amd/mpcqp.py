@@ -32,7 +32,7 @@ class MpcParams(C.Structure):
         ("lane_width", C.c_double), ("safe_lane_margin", C.c_double),
         ("brake_distance", C.c_double), ("brake_accel", C.c_double),
         ("linearization", C.c_int), ("sqp_iters", C.c_int), ("max_iter", C.c_int), ("polish", C.c_int),
-        ("tol", C.c_double), ("tol_mu", C.c_double), ("elastic_rho", C.c_double),
+        ("tol", C.c_double), ("tol_mu", C.c_double), ("elastic_rho", C.c_double), ("sqp_tol", C.c_double),
     ]
 
 

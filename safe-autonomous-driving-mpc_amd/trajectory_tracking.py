@@ -11,9 +11,13 @@ Reference: medinammartin3/Safe-Autonomous-Driving-MPC trajectory_tracking.py
   run_simulation     (:377-443)  same loop and returned histories, plus an optional step cap.
 
 What differs by design: the reference's SLSQP on the nonlinear problem
-(ftol 1e-3, maxiter 15, finite-difference gradients) is replaced by the Gauss-Newton QP at the
-same warm start, solved to 1e-9 by a primal-dual interior point on the GPU (`sqp_iters` > 1
-re-linearises).  There is no CPU fallback: without libmpcqp.so or a GPU, solve() raises.
+(ftol 1e-3, maxiter 15, finite-difference gradients) is replaced by a Gauss-Newton SQP from the
+same warm start: each QP is solved to 1e-9 by a primal-dual interior point on the GPU and re-linearised
+about its solution until U moves by at most `sqp_tol` (at most `sqp_iters` QPs).  By default solve()
+therefore returns the optimum of the reference's own nonlinear problem (pinned to it by
+tests/golden/nlp_golden.npz), which its SLSQP only approximates; `sqp_iters = 1` gives the single
+tracking QP at the warm start that bench.py times.  There is no CPU fallback: without libmpcqp.so or a
+GPU, solve() raises.
 """
 import time
 
@@ -22,11 +26,14 @@ import numpy as np
 import mpcqp
 from sanity_checks import trajectory_tracking_check
 
+# Gauss-Newton SQP cap of the drop-in default (sqp_tol stops it earlier, typically after 4-7 QPs)
+SQP_ITERS = 10
+
 # TrajectoryTracker attribute -> mpc_params field
 _PARAM_ATTRS = ("dt", "N", "vehicle_radius", "w_d", "w_o", "w_v", "w_u1", "w_u2", "obstacle_safety_distance",
                 "max_time_2_obs", "wheelbase", "lane_width", "safe_lane_margin")
 _SOLVER_ATTRS = ("linearization", "sqp_iters", "max_iter", "polish", "tol", "tol_mu", "elastic_rho",
-                 "brake_distance", "brake_accel")
+                 "brake_distance", "brake_accel", "sqp_tol")
 
 
 class TrajectoryTracker:
@@ -51,9 +58,11 @@ class TrajectoryTracker:
         self.wheelbase = 2.8
         self.lane_width = 3.0
         self.safe_lane_margin = 0.1
-        # GPU QP solver knobs (defaults of mpc_default_params)
+        # GPU solver knobs.  The SQP defaults make solve() return the optimum of the reference's nonlinear
+        # problem (nlp_golden); the other values are those of mpc_default_params
         self.linearization = 1
-        self.sqp_iters = 1
+        self.sqp_iters = SQP_ITERS
+        self.sqp_tol = 1e-10
         self.max_iter = 80
         self.polish = 2
         self.tol = 1e-9
@@ -253,11 +262,24 @@ def run_simulation(mpc, fsm, trajectory, max_steps=None, verbose=True):
         car = [o["s"] for o in obstacles if o["type"] == "car"]
         hist_obs_s.append(car[0] if car else np.nan)
         if verbose and step % 50 == 0:
-            print(f"Step {step} | s={x[0]:.1f}m, v={x[4] * 3.6:.1f}km/h | status={mpc.last_status}")
+            print(progress_line(step, x, tl_state, hist_obs_s[-1], fsm, mpc.obstacle_safety_distance))
         step += 1
     trajectory_tracking_check(mpc, hist_x, hist_u, hist_t, hist_obs_s, hist_tl_state, fsm, trajectory.s_max)
     return (np.array(hist_x), np.array(hist_u), np.array(hist_t), hist_preds, hist_obs_s, hist_tl_state,
             trajectory)
+
+
+def progress_line(step, x, tl_state, obstacle_s, fsm, safety_distance=5.0):
+    """The reference's progress print of run_simulation (trajectory_tracking.py:423-435), verbatim format."""
+    vehicle_info = f"s={x[0]:.1f}m, v={x[4] * 3.6:.1f}km/h"
+    if fsm.traffic_light:
+        dist_2_tl = fsm.tl_pos - x[0]
+        tl_info = (f"color={tl_state}, distance={dist_2_tl:.1f}m" if dist_2_tl > safety_distance
+                   else f"color={tl_state}, distance=NaN")
+    else:
+        tl_info = "NaN"
+    obs_info = f"{obstacle_s - x[0]:.1f}m" if not np.isnan(obstacle_s) else "NaN"
+    return f"Step {step} | {vehicle_info} | Traffic Light : {tl_info} | Distance to obstacle : {obs_info}"
 
 
 def fsm_params(fsm):

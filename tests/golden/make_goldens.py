@@ -671,15 +671,223 @@ def gen_solve():
 
 
 # ----------------------------------------------------------------------------------------
+# 5b. tight NLP optimum of the reference's own problem ("Tight NLP optimum")
+# ----------------------------------------------------------------------------------------
+def _central_jac(fun, x, h=1e-4):
+    """Fourth-order central finite differences of a vector (or scalar) function of the reference:
+    (-f(x+2h) + 8 f(x+h) - 8 f(x-h) + f(x-2h)) / 12h.  Its rounding noise (~eps |f| / h) is what limits
+    the certificates below on the high-cost obstacle cases (|f| ~ 1e3); the h^4 truncation is negligible."""
+    f0 = np.atleast_1d(fun(x))
+    J = np.zeros((f0.size, x.size))
+    for j in range(x.size):
+        e = np.zeros(x.size)
+        e[j] = h
+        f = lambda t: np.atleast_1d(fun(x + t * e))
+        J[:, j] = (-f(2) + 8 * f(1) - 8 * f(-1) + f(-2)) / (12 * h)
+    return J
+
+
+def split_constraints(tr, x0, obs):
+    """The reference's constraint function (trajectory_tracking.py:155-211) with each obstacle row
+    s_o + v_o k dt - s - max(5, 1.5 v) >= 0 (:194-204) written as its two smooth rows (- 5 and - 1.5 v):
+    the same feasible set without the kink of max() that stops SLSQP's line search (status 8) whenever an
+    obstacle row is active at v = 5 / 1.5.  Rows are taken from the reference's own output."""
+    base = tr.constraints(x0, obs)["fun"]
+    if not obs:
+        return base
+    per = 7 + len(obs)
+    osd, tg = tr.obstacle_safety_distance, tr.max_time_2_obs
+
+    def g(U):
+        c = base(U)
+        X = tr.predict(x0, U)
+        out = []
+        for k in range(tr.N):
+            blk = c[k * per:(k + 1) * per]
+            v = X[k + 1, 4]
+            m = max(osd, v * tg)
+            out.extend(blk[:6])
+            for i in range(len(obs)):
+                out.append(blk[6 + i] + m - osd)
+                out.append(blk[6 + i] + m - v * tg)
+            out.append(blk[-1])
+        return np.array(out)
+    return g
+
+
+def nlp_kkt(tr, ld, x0, obs, U, act_tol=1e-7):
+    """KKT check of the reference NLP (cost :116-152, constraints :155-211 in the split form, bounds :249)
+    at U with central-FD derivatives of the reference functions: multipliers of the active rows by
+    non-negative least squares (stationarity `stat`, relative to 1 + |grad|), and `err_est`, the
+    length of the equality-constrained Newton step on the active set with the Gauss-Newton Hessian of
+    build_qp at U -- an estimate of the distance of U to the local optimum, in U units."""
+    from scipy.optimize import nnls
+    N = tr.N
+    g = _central_jac(lambda u: tr.cost(u, x0), U)[0]
+    cf = split_constraints(tr, x0, obs)
+    c = cf(U)
+    A = _central_jac(cf, U)
+    lo = np.tile(tr.u_min, N)
+    hi = np.tile(tr.u_max, N)
+    rows, rhs = [], []
+    for i in np.flatnonzero(c <= act_tol):
+        rows.append(A[i]); rhs.append(c[i])
+    for j in np.flatnonzero(U - lo <= act_tol):
+        rows.append(np.eye(2 * N)[j]); rhs.append(U[j] - lo[j])
+    for j in np.flatnonzero(hi - U <= act_tol):
+        rows.append(-np.eye(2 * N)[j]); rhs.append(hi[j] - U[j])
+    n = 2 * N
+    H = build_qp(tr, ld, x0, obs, U)["H"]
+    if rows:
+        Aa = np.array(rows)
+        lam, _ = nnls(Aa.T, g, maxiter=5000)
+        res = g - Aa.T @ lam
+        na = len(rows)
+        K = np.zeros((n + na, n + na))
+        K[:n, :n] = H
+        K[:n, n:] = -Aa.T
+        K[n:, :n] = Aa
+        sol = np.linalg.lstsq(K, np.concatenate([-g, -np.array(rhs)]), rcond=None)[0]
+        du = sol[:n]
+    else:
+        lam = np.zeros(0)
+        res = g
+        du = np.linalg.solve(H, -g)
+    return dict(stat=float(np.abs(res).max() / (1.0 + np.abs(g).max())), prim=float(max(0.0, -c.min(initial=0.0))),
+                n_active=len(rows), lam_max=float(lam.max(initial=0.0)), err_est=float(np.abs(du).max()))
+
+
+def solve_nlp_case(args):
+    """One reference NLP, solved twice:
+      stage 1 = SURVEY App. C exactly: minimize(cost, ubar, SLSQP, bounds, constraints), ftol 1e-12,
+                maxiter 1000, scipy's 2-point finite-difference derivatives (the reference's solve(),
+                trajectory_tracking.py:254-256, only tighter);
+      stage 2 = continuation from stage 1 on the same reference functions with the obstacle rows split
+                (split_constraints) and central-FD derivatives (2-point FD limits stage 1 to ~1e-5 in U,
+                and the max() kink stops its line search).
+    `certified` = stage 2 converged (SLSQP status 0) to a feasible point whose KKT check (nlp_kkt) puts it
+    within 1e-7 of the local optimum."""
+    ti, N, ok, seed = args
+    rng = np.random.default_rng(seed)
+    ld = loader(ti)
+    tr = tracker(ti, N)
+    x0 = draw_x0(ld, rng)
+    obs = draw_obstacles(ok, x0, rng)
+    ubar = capture_warmstart(tr, x0, obs)
+    cons = tr.constraints(x0, obs)
+    bounds = [(tr.u_min[0], tr.u_max[0]), (tr.u_min[1], tr.u_max[1])] * N
+    t0 = time.time()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        r1 = sp_minimize(tr.cost, ubar, args=(x0,), method="SLSQP", bounds=bounds, constraints=cons,
+                         options={"ftol": 1e-12, "maxiter": 1000})
+        t1 = time.time() - t0
+        sg = split_constraints(tr, x0, obs)
+        cons2 = {"type": "ineq", "fun": sg, "jac": lambda u: _central_jac(sg, u)}
+        r2 = sp_minimize(tr.cost, r1.x, args=(x0,), jac=lambda u, x: _central_jac(lambda v: tr.cost(v, x), u)[0],
+                         method="SLSQP", bounds=bounds, constraints=cons2, options={"ftol": 1e-15, "maxiter": 150})
+    k1 = nlp_kkt(tr, ld, x0, obs, r1.x)
+    U, kk, stage, n3 = r2.x, nlp_kkt(tr, ld, x0, obs, r2.x), 2, 0
+    if not (kk["prim"] <= 1e-9 and kk["err_est"] <= 1e-8):
+        U3, n3 = fd_sqp(tr, ld, x0, obs, r2.x)
+        k3 = nlp_kkt(tr, ld, x0, obs, U3)
+        if k3["prim"] <= max(kk["prim"], 1e-9) and k3["err_est"] < kk["err_est"]:
+            U, kk, stage = U3, k3, 3
+    feasible = bool(kk["prim"] <= 1e-9)
+    certified = bool(feasible and kk["err_est"] <= 1e-6 and kk["stat"] <= 1e-6)
+    return dict(traj=ti, N=N, x0=x0, obs=np.array([[o["s"], o["v"]] for o in obs]).reshape(-1, 2), ubar=ubar,
+                U_nlp=U, U_slsqp=r1.x, nit1=r1.nit, status1=r1.status, nit2=r2.nit, status2=r2.status, stage=stage,
+                nit3=n3, fun=float(tr.cost(U, x0)), fun_slsqp=float(r1.fun), feasible=feasible, certified=certified,
+                kkt=json.dumps(kk), kkt_slsqp=json.dumps(k1), seconds=time.time() - t0, seconds1=t1)
+
+
+def fd_sqp(tr, ld, x0, obs, U, iters=25):
+    """Stage 3, used when SLSQP stops short (status 8 on degenerate or kinked problems): Newton-type SQP
+    on the reference's own functions, golden-side -- gradient and constraint Jacobian by central FD of
+    cost() and the split constraints, the Gauss-Newton Hessian of build_qp, each QP solved exactly by
+    active_set_polish.  Stops when the step is below 1e-12."""
+    N = tr.N
+    n = 2 * N
+    cf = split_constraints(tr, x0, obs)
+    lo = np.tile(tr.u_min, N)
+    hi = np.tile(tr.u_max, N)
+    U = np.clip(np.array(U, np.float64), lo, hi)
+    best, best_step = U.copy(), np.inf
+    for it in range(iters):
+        g = _central_jac(lambda u: tr.cost(u, x0), U)[0]
+        c = cf(U)
+        A = _central_jac(cf, U)
+        H = build_qp(tr, ld, x0, obs, U)["H"]
+        Aall = np.vstack([A, np.eye(n), -np.eye(n)])
+        b = np.concatenate([-c, lo - U, U - hi])
+        d, _, ok, _ = active_set_polish(H, g, Aall, b, np.zeros(len(b), bool), RHO_DEFAULT, np.zeros(n), True)
+        step = float(np.abs(d).max())
+        if step < best_step:            # past the FD noise floor the steps jitter: keep the calmest point
+            best, best_step = U.copy(), step
+        U = np.clip(U + d, lo, hi)
+        if step < 1e-12:
+            return U, it + 1
+    return best, iters
+
+
+NLP_PLAN = [  # (traj, N, obstacle kind, count): the C1-C5 shapes plus the reference default N=5
+    (1, 10, 0, 10), (1, 20, 0, 12), (2, 20, "fsm", 12), (3, 30, 2, 10), (3, 40, 8, 8), (2, 5, "fsm", 8),
+]
+
+
+def gen_nlp(procs=8):
+    import multiprocessing as mp
+    jobs = []
+    seed = 7700
+    for (ti, N, ok, cnt) in NLP_PLAN:
+        for _ in range(cnt):
+            jobs.append((ti, N, ok, seed))
+            seed += 1
+    t0 = time.time()
+    with mp.get_context("fork").Pool(procs) as pool:
+        cases = []
+        for c in pool.imap(solve_nlp_case, jobs):
+            cases.append(c)
+            k = json.loads(c["kkt"])
+            print(f"  nlp case {len(cases)} traj{c['traj']} N={c['N']} obs={len(c['obs'])} feasible={c['feasible']} "
+                  f"certified={c['certified']} nit={c['nit1']}+{c['nit2']} st={c['status1']},{c['status2']} "
+                  f"err_est={k['err_est']:.1e} stat={k['stat']:.1e} prim={k['prim']:.1e} "
+                  f"|U_slsqp-U|={np.abs(c['U_slsqp'] - c['U_nlp']).max():.1e} ({time.time()-t0:.0f}s)", flush=True)
+    out = {"n": np.array(len(cases))}
+    for j, c in enumerate(cases):
+        for k, v in c.items():
+            out[f"c{j}_{k}"] = np.asarray(v)
+    save("nlp_golden", **out)
+
+
+# ----------------------------------------------------------------------------------------
 # 6. closed loop (run_simulation) histories
 # ----------------------------------------------------------------------------------------
 def gen_closedloop():
     out = {}
-    runs = [("c1_traj1_N10", 1, 10, False, False), ("traj2_N5_fsm", 2, 5, True, True)]
+    runs = [("c1_traj1_N10", 1, 10, False, False), ("traj2_N5_fsm", 2, 5, True, True),
+            ("traj3_N5_fsm", 3, 5, True, True)]
+    if os.environ.get("CL_ONLY"):
+        runs = [r for r in runs if r[0] in os.environ["CL_ONLY"].split(",")]
+        old = os.path.join(HERE, "closedloop_golden.npz")
+        if os.path.exists(old):
+            with np.load(old, allow_pickle=False) as z:
+                out.update({k: z[k] for k in z.files if k != "meta_json"})
     for (tag, ti, N, dyn, tl) in runs:
         ld = loader(ti)
         tr = tracker(ti, N)
         fsm = RT.ObstaclesFSM(dynamic_obstacle=dyn, traffic_light=tl)
+        if ti == 3:
+            # the trajectory3 preset, commented out in the reference (trajectory_tracking.py:311-327);
+            # SURVEY Appendix C: overwrite the attributes of the active (trajectory2) preset
+            fsm.obs_trigger_s = 5.0
+            fsm.obs_start_s = fsm.obs_s = 150.0
+            fsm.obs_v = 4.0
+            fsm.obs_end_s = 850.0
+            fsm.tl_pos = 2000.0
+            fsm.tl_trigger_s = 100.0
+            fsm.tl_stop_duration = 20.0
         t0 = time.time()
         buf = io.StringIO()
         with contextlib.redirect_stdout(buf):
@@ -704,7 +912,8 @@ def main():
     todo = a.only.split(",") if a.only else ["convert", "interp", "pose", "model", "warmstart", "qpdata", "qp",
                                               "solve", "closedloop"]
     fns = dict(convert=convert_trajectories, interp=gen_interp, pose=gen_pose, model=gen_model, warmstart=gen_warmstart,
-               qpdata=gen_qpdata, qp=lambda: gen_qp(a.quick), solve=gen_solve, closedloop=gen_closedloop)
+               qpdata=gen_qpdata, qp=lambda: gen_qp(a.quick), solve=gen_solve, closedloop=gen_closedloop,
+               nlp=gen_nlp)
     for t in todo:
         print(f"== {t}")
         fns[t]()

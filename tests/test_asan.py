@@ -1,0 +1,157 @@
+"""Sanitizer runs of the host-only code ("an ASan/UBSan build of the CPU C++ path in tests").
+
+tests/asan/Makefile builds, with -fsanitize=address,undefined (every report fatal):
+  json_driver    csrc/host_table.h -- the native trajectory JSON reader (replaces the json.load of
+                 trajectory_loader.py:13-24), the device-table build (:26-84) and the bucketed interval
+                 search restated from the device's seg_t;
+  oracle_driver  oracle/mpc_oracle.c -- the CPU restatement.
+The reader runs over the reference trajectories (regenerated from the package data, verbatim floats) and a
+malformed / duplicate-key / deeply nested corpus; every answer must match Python's json.load (the
+reference's loader).  The oracle driver's results must equal the regular build's bit for bit.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, traj_arrays
+
+ASAN = os.path.join(ROOT, "tests", "asan")
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:abort_on_error=0",
+           UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+
+
+@pytest.fixture(scope="module")
+def drivers():
+    r = subprocess.run(["make", "-C", ASAN], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return os.path.join(ASAN, "json_driver"), os.path.join(ASAN, "oracle_driver")
+
+
+def traj_json(i):
+    X, U = traj_arrays(i)
+    return json.dumps({"X": X.tolist(), "U": U.tolist(), "S": list(range(len(U)))})
+
+
+def run_json(drv, files):
+    r = subprocess.run([drv] + [str(f) for f in files], capture_output=True, text=True, env=ENV, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+    return r.stdout.splitlines()
+
+
+def expect_line(text):
+    """What json.load makes of the text, in the driver's output format (status only for errors)."""
+    try:
+        d = json.loads(text)
+        X = np.asarray(d["X"], np.float64).reshape(-1, 5)
+        U = np.asarray(d["U"], np.float64).reshape(-1, 2)
+    except Exception:
+        return "ERR"
+    return ("OK", X.shape[0], U.shape[0], X, U)
+
+
+def test_json_reader_reference_trajectories(drivers, tmp_path):
+    files = []
+    for i in (1, 2, 3):
+        f = tmp_path / f"trajectory{i}.json"
+        f.write_text(traj_json(i))
+        files.append(f)
+    out = run_json(drivers[0], files)
+    for i, line in zip((1, 2, 3), out):
+        tag, T, Tu, sx, su, bad = line.split()
+        X, U = traj_arrays(i)
+        assert tag == "OK" and int(T) == X.shape[0] and int(Tu) == U.shape[0]
+        assert abs(float(sx) - X.sum()) <= 1e-9 * abs(X).sum() and abs(float(su) - U.sum()) <= 1e-9 * abs(U).sum()
+        assert int(bad) == 0          # bucketed search == lower_bound everywhere
+
+
+def corpus():
+    X, U = traj_arrays(1)
+    xs, us = json.dumps(X[:6].tolist()), json.dumps(U[:5].tolist())
+    x2 = json.dumps(X[:9].tolist())
+    deep = "[" * 100000 + "]" * 100000
+    return {
+        "dup_X_last_wins": '{"X": %s, "U": %s, "X": %s}' % (xs, us, x2),         # 9 rows, json.load: last
+        "dup_X_shorter_last": '{"X": %s, "U": %s, "X": %s}' % (x2, us, xs),
+        "dup_U": '{"U": [[1,2],[3,4],[5,6]], "X": %s, "U": %s}' % (xs, us),
+        "deep_nesting_skipped_key": '{"deep": %s, "X": %s, "U": %s}' % (deep, xs, us),
+        "nested_ok": '{"meta": {"a": [1, {"b": [true, false, null, "s\\"t"]}]}, "X": %s, "U": %s}' % (xs, us),
+        "unicode_key": '{"\\u0058": %s, "U": %s}' % (xs, us),
+        "truncated": '{"X": %s, "U": [[1, 2], [3' % xs,
+        "wrong_width": '{"X": [[1,2,3,4]], "U": %s}' % us,
+        "trailing_data": '{"X": %s, "U": %s} extra' % (xs, us),
+        "missing_U": '{"X": %s}' % xs,
+        "empty_object": "{}",
+        "empty_file": "",
+        "not_object": "[1, 2, 3]",
+        "hex_number": '{"X": [[0x10, 1, 2, 3, 4]], "U": %s}' % us,
+        "inf_word": '{"X": [[inf, 1, 2, 3, 4]], "U": %s}' % us,
+        "nan_json": '{"X": [[NaN, 1, 2, 3, -Infinity]], "U": [[1, 2], [Infinity, 3]]}',
+        "unterminated_string": '{"X": %s, "U": %s, "note": "abc' % (xs, us),
+        "bad_escape": '{"\\u00zz": 1, "X": %s, "U": %s}' % (xs, us),
+        "garbage_bytes": "\x00\xff{\x01",
+    }
+
+
+def test_json_reader_malformed_corpus(drivers, tmp_path):
+    items = corpus()
+    files = []
+    for name, text in items.items():
+        f = tmp_path / f"{name}.json"
+        f.write_text(text, encoding="latin-1")
+        files.append(f)
+    out = run_json(drivers[0], files)
+    assert len(out) == len(items)
+    for (name, text), line in zip(items.items(), out):
+        exp = expect_line(text)
+        if exp == "ERR":
+            assert line.startswith("ERR"), (name, line)
+            continue
+        tag, T, Tu, sx, su, bad = line.split()
+        assert tag == "OK", (name, line)
+        assert (int(T), int(Tu)) == (exp[1], exp[2]), (name, line)
+        assert np.isclose(float(sx), np.sum(exp[3]), equal_nan=True), (name, line)
+        assert np.isclose(float(su), np.sum(exp[4]), equal_nan=True), (name, line)
+    got = dict(zip(items, out))
+    assert got["dup_X_last_wins"].split()[1] == "9" and got["dup_X_shorter_last"].split()[1] == "6"
+    assert "nesting too deep" in got["deep_nesting_skipped_key"]
+
+
+def _oracle_inputs(B, kind, seed):
+    import workloads as W
+    cfg = {0: "C2", "fsm": "C3", 8: "C5"}[kind]
+    wb = W.make_batch(cfg, B=B, seed=seed)
+    X, U = traj_arrays(wb["traj"])
+    mo = wb["max_obs"]
+    obs = wb["obs"] if mo else np.zeros((B, 0, 2))
+    nob = wb["n_obs"] if mo else np.zeros(B, np.int32)
+    return X, U, wb["x0"], obs, nob.astype(np.int32), mo, wb["traj"], wb["N"]
+
+
+@pytest.mark.parametrize("kind,B,sqp", [(0, 48, 1), ("fsm", 32, 10), (8, 12, 1)])
+def test_oracle_under_asan_matches_regular_build(drivers, tmp_path, kind, B, sqp):
+    import oracle as O
+    X, U, x0, obs, nob, mo, ti, N = _oracle_inputs(B, kind, 5)
+    fin = tmp_path / "in.bin"
+    with open(fin, "wb") as f:
+        f.write(np.array([X.shape[0], U.shape[0], N, B, mo, sqp], np.int32).tobytes())
+        for a in (X, U, x0, obs):
+            f.write(np.ascontiguousarray(a, np.float64).tobytes())
+        f.write(np.ascontiguousarray(nob, np.int32).tobytes())
+    fout = tmp_path / "out.bin"
+    r = subprocess.run([drivers[1], str(fin), str(fout)], capture_output=True, text=True, env=ENV, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "runtime error" not in r.stderr, r.stderr[-3000:]
+    raw = fout.read_bytes()
+    nU, nX = B * 2 * N, B * 5 * (N + 1)
+    Ua = np.frombuffer(raw[:8 * nU], np.float64).reshape(B, N, 2)
+    Xa = np.frombuffer(raw[8 * nU:8 * (nU + nX)], np.float64).reshape(B, N + 1, 5)
+    sa = np.frombuffer(raw[8 * (nU + nX):], np.int32)[:B]
+    orc = O.Oracle(X, U)
+    ro = orc.solve_batch(O.default_params(N=N, max_obs=mo, sqp_iters=sqp), x0, obs if mo else None,
+                         nob if mo else None)
+    assert np.array_equal(sa, ro["status"])
+    assert np.array_equal(Ua, ro["U"]) and np.array_equal(Xa, ro["Xpred"])

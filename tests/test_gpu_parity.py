@@ -3,9 +3,11 @@ and the CPU oracle.  Tolerances:
   lookups, warm start, nominal rollout / predict: bit-exact (FP64 integer-free arithmetic
       identical to numpy; the kernel is compiled with -ffp-contract=off);
   QP(ubar) solution U*: <= 5e-8 abs vs the KKT-certified golden (the BASELINE gate is 1e-5)
-      and <= 1e-6 vs the oracle's PDIP on seeded batches of every configuration (measured
-      4.8e-13 on the full C2 batch); status flips only between infeasible/numerical on badly
-      infeasible elastic problems, checked by objective value (check_vs_oracle).
+      and <= 1e-9 vs the oracle (same warm start, QP and solver) on the FULL per-GPU batch of every
+      configuration (measured round 2: 4.8e-13 on C2, 5.6e-11 on C5); statuses identical, except flips
+      between infeasible/numerical on badly infeasible elastic problems, and elastic instances where the
+      two sides certified different points of the same elastic optimum: both checked by objective value
+      (check_vs_oracle) and counted in the printed summary.
 """
 import json
 
@@ -16,7 +18,7 @@ from conftest import golden_cases, load_golden, traj_arrays
 
 pytestmark = pytest.mark.gpu
 
-TOL_U = 1e-6          # GPU vs oracle (same PDIP); tightened once the active-set polish lands
+TOL_U = 1e-9          # GPU vs oracle (same warm start, QP, PDIP and polish)
 TOL_GATE = 1e-5       # BASELINE.json parity gate vs the certified golden
 TOL_CERT = 5e-8       # what the solver actually reaches vs the certified golden (oracle: 9.8e-9)
 
@@ -144,50 +146,66 @@ def elastic_objective(orc, p, x0, obs, U):
     return 0.5 * du @ q["H"] @ du + q["f"] @ du + q["c0"] + p.elastic_rho * viol.sum()
 
 
-def check_vs_oracle(r, ro, min_agree=0.99, ctx=None):
-    """Status agreement and U/Xpred parity.  Statuses may only differ between infeasible (2) and
-    numerical (3) -- both mean "no certified solution of the hard QP".  These flips happen on badly
-    infeasible elastic problems (rho = 1e5), where the last interior-point iterates of the two
-    implementations differ by rounding; for each flip the side that certified its elastic optimum
-    (status 2, KKT-checked by the polish) must have an objective no worse than the other side's.
-    U is compared wherever both sides certified a solution."""
+def check_vs_oracle(r, ro, ctx=None, label=""):
+    """Status and U/Xpred parity, returns the summary dict (printed by the callers).
+    Statuses must agree, except flips between infeasible (2) and numerical (3): both mean "no certified
+    solution of the hard QP"; they happen on badly infeasible elastic problems (rho = 1e5), where the last
+    interior-point iterates of the two implementations differ by rounding, and the side that certified
+    its elastic optimum (status 2, KKT-checked by the polish) must have an objective no worse than the
+    other's.  U must agree to TOL_U wherever both sides certified a solution, except on elastic instances
+    (status 2 on both) whose two answers have the same elastic objective to 1e-9 relative: the polish can
+    certify two points of one flat elastic optimum ("Elastic-problem tolerance")."""
     agree = r["status"] == ro["status"]
     mism = ~agree
     assert np.isin(r["status"][mism], (2, 3)).all() and np.isin(ro["status"][mism], (2, 3)).all(), \
-        (r["status"][mism], ro["status"][mism])
+        (label, r["status"][mism], ro["status"][mism])
+    orc = p = x0 = obs = n_obs = None
     if ctx is not None:
         orc, p, x0, obs, n_obs = ctx
-        for i in np.flatnonzero(mism):
-            o = None if obs is None else obs[i, :n_obs[i]]
-            fg = elastic_objective(orc, p, x0[i], o, r["U"][i])
-            fo = elastic_objective(orc, p, x0[i], o, ro["U"][i])
-            cert, other = (fg, fo) if r["status"][i] == 2 else (fo, fg)
-            assert cert <= other + 1e-6 * (1.0 + abs(other)), (i, fg, fo, r["status"][i], ro["status"][i])
-    assert agree.mean() >= min_agree, (agree.mean(), np.flatnonzero(~agree)[:10])
+    obj = lambda i, U: elastic_objective(orc, p, x0[i], None if obs is None else obs[i, :n_obs[i]], U)
+    for i in np.flatnonzero(mism):
+        assert ctx is not None, (label, "status flip without context", i)
+        fg, fo = obj(i, r["U"][i]), obj(i, ro["U"][i])
+        cert, other = (fg, fo) if r["status"][i] == 2 else (fo, fg)
+        assert cert <= other + 1e-6 * (1.0 + abs(other)), (label, i, fg, fo, r["status"][i], ro["status"][i])
     cert = np.isin(r["status"], (0, 2)) & np.isin(ro["status"], (0, 2))
     err = np.abs(r["U"] - ro["U"]).reshape(len(cert), -1).max(axis=1)
-    assert err[cert].max(initial=0.0) <= TOL_U, (err[cert].max(), np.flatnonzero(cert & (err > TOL_U))[:10])
+    alt = 0
+    for i in np.flatnonzero(cert & (err > TOL_U)):
+        assert ctx is not None and r["status"][i] == 2 and ro["status"][i] == 2, \
+            (label, i, err[i], r["status"][i], ro["status"][i])
+        fg, fo = obj(i, r["U"][i]), obj(i, ro["U"][i])
+        assert abs(fg - fo) <= 1e-9 * (1.0 + abs(fo)), (label, i, err[i], fg, fo)
+        alt += 1
+    ok = cert & (err <= TOL_U)
     xe = np.abs(r["Xpred"] - ro["Xpred"]).reshape(len(cert), -1).max(axis=1)
-    assert xe[cert].max(initial=0.0) <= 1e-6
+    assert xe[ok].max(initial=0.0) <= 1e-8, (label, xe[ok].max())
+    s = dict(label=label, B=len(cert), status_agree=float(agree.mean()), flips_2_3=int(mism.sum()),
+             elastic_alt_optima=alt, max_err_U=float(err[ok].max(initial=0.0)),
+             max_err_Xpred=float(xe[ok].max(initial=0.0)))
+    print(json.dumps(s))
+    return s
 
 
-@pytest.mark.parametrize("cfg,B", [("C1", 64), ("C2", 512), ("C3", 512), ("C4", 256), ("C5", 128)])
-def test_vs_oracle_seeded(lib, solvers, cfg, B):
-    """Seeded batches of every BASELINE configuration: GPU == oracle (warm start + QP + predict)."""
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
+def test_vs_oracle_full_batch(lib, solvers, cfg):
+    """The full per-GPU batch of every BASELINE configuration (bench.py's inputs: C2 4096, C3 8192,
+    C4 4096, C5 8192; C1 64 egos): GPU == oracle (warm start + QP + predict) to TOL_U."""
     import oracle as O
     import workloads as W
-    wb = W.make_batch(cfg, B=B, seed=1234)
+    B = 64 if cfg == "C1" else W.CONFIGS[cfg]["B"] // W.CONFIGS[cfg]["gpus"]
+    wb = W.make_batch(cfg, B=B)
     slv = solvers[wb["traj"]]
     set_p(lib, slv, wb["N"], wb["max_obs"])
     r = slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
     orc = O.Oracle(*traj_arrays(wb["traj"]))
     po = O.default_params(N=wb["N"], max_obs=wb["max_obs"])
     ro = orc.solve_batch(po, wb["x0"], wb["obs"], wb["n_obs"])
-    check_vs_oracle(r, ro, min_agree=0.97, ctx=(orc, po, wb["x0"], wb["obs"], wb["n_obs"]))
+    check_vs_oracle(r, ro, ctx=(orc, po, wb["x0"], wb["obs"], wb["n_obs"]), label=f"{cfg} B={B}")
     assert np.array_equal(r["u0"], r["U"][:, 0, :])
 
 
-@pytest.mark.parametrize("cfg,B,nsqp", [("C2", 256, 3), ("C3", 256, 2)])
+@pytest.mark.parametrize("cfg,B,nsqp", [("C2", 4096, 3), ("C3", 2048, 10), ("C4", 1024, 10)])
 def test_sqp_relinearisation_vs_oracle(lib, solvers, cfg, B, nsqp):
     """SQP outer iterations on device: QP(U*) re-linearised about the previous
     solution, `sqp_iters` times; same fixed-point path as the oracle's orc_solve loop."""
@@ -200,7 +218,7 @@ def test_sqp_relinearisation_vs_oracle(lib, solvers, cfg, B, nsqp):
     orc = O.Oracle(*traj_arrays(wb["traj"]))
     po = O.default_params(N=wb["N"], max_obs=wb["max_obs"], sqp_iters=nsqp)
     ro = orc.solve_batch(po, wb["x0"], wb["obs"], wb["n_obs"])
-    check_vs_oracle(r, ro, min_agree=0.97)
+    check_vs_oracle(r, ro, label=f"SQP {cfg} K={nsqp}")
     assert (r["iters"] >= 0).all()
 
 
@@ -220,10 +238,9 @@ def test_full_size_C2_properties(lib, solvers):
     # deterministic: same inputs -> bit-identical outputs
     r2 = slv.solve_batch(wb["x0"])
     assert np.array_equal(r["U"], r2["U"]) and np.array_equal(r["iters"], r2["iters"])
-    idx = np.random.default_rng(0).choice(4096, 256, replace=False)
     orc = O.Oracle(*traj_arrays(1))
-    ro = orc.solve_batch(O.default_params(N=20), wb["x0"][idx])
-    assert np.abs(r["U"][idx] - ro["U"]).max() <= TOL_U
+    ro = orc.solve_batch(O.default_params(N=20), wb["x0"])
+    assert np.abs(r["U"] - ro["U"]).max() <= TOL_U
 
 
 def test_edge_cases(lib, solvers):
@@ -248,7 +265,7 @@ def test_edge_cases(lib, solvers):
         po = O.default_params(N=N, max_obs=mo)
         ro = orc.solve_batch(po, x0s, obs, n)
         # instance 5 (obstacle 4 m ahead at 12 m/s) is the badly infeasible elastic case of check_vs_oracle
-        check_vs_oracle(r, ro, min_agree=5 / 6, ctx=(orc, po, x0s, obs, n))
+        check_vs_oracle(r, ro, ctx=(orc, po, x0s, obs, n), label=f"edge N={N}")
         assert np.isfinite(r["Xpred"]).all()
     # obstacle inside 5 m: infeasible, still returns a control (the reference always returns one)
     assert r["status"][2] == 2 and r["status"][3] == 2
@@ -270,10 +287,10 @@ def test_shim_solve_matches_oracle(lib):
     obs = [{"s": 730.0, "v": 4.0, "type": "car"}, {"s": 760.0, "v": 0.0, "type": "light"}]
     u0, pred_X, t = mpc.solve(x0, obs)
     orc = O.Oracle(traj.X_ref, traj.U_ref)
-    ro = orc.solve(O.default_params(N=20, max_obs=2), x0, [(730.0, 4.0), (760.0, 0.0)])
+    ro = orc.solve(O.default_params(N=20, max_obs=2, sqp_iters=TT.SQP_ITERS), x0, [(730.0, 4.0), (760.0, 0.0)])
     assert pred_X.shape == (21, 5) and u0.shape == (2,)
     assert np.abs(u0 - ro["u0"]).max() <= TOL_U
-    assert np.abs(pred_X - ro["Xpred"]).max() <= 1e-6
+    assert np.abs(pred_X - ro["Xpred"]).max() <= 1e-8
     assert t >= 0.0 and mpc.last_status == ro["status"]
 
 
