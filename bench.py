@@ -137,13 +137,24 @@ def main():
     flops = algorithmic_flops(N, kmean) * B
     rflops = riccati_flops(N, kmean) * B
     nbytes = algorithmic_bytes(N, mo) * B
-    traffic = None
+    # PMC counters cannot be read inside this process (rocprofv3 collects them in their own runs,
+    # tools/gpu_bench_prof.sh); `traffic` is the per-step HBM bytes of the last such run of this config,
+    # reported with the run it came from
+    traffic, traffic_source = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_hbm_bytes.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(args.config)
+            pj = json.load(open(pmc))
+            traffic = pj.get(args.config)
+            d = pj.get(args.config + "_detail", {})
+            traffic_source = {"file": "profiles/pmc_hbm_bytes.json", "round": d.get("round"),
+                              "commit": d.get("commit"), "counters": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                              "(separate passes), 2*FETCH_SIZE + WRITE_SIZE per step"}
         except Exception:
             traffic = None
+
+    # closed-loop leg on every rank (its own ego shard), one gather to rank 0; after the headline timing
+    cl = closed_loop(args.config, args.closed_loop, N, local, world, rank, dev) if args.closed_loop else None
 
     if rank == 0:
         out = {
@@ -164,12 +175,12 @@ def main():
                                    f"max_obs={mo}, seed {cfg['seed']} (SURVEY 8d)", "global_batch": world * B,
                        "horizon": N, "parallelism": f"dp{world} (ego shards)"},
             "solver": tel,
-            "roofline": {"bound": "mfma", "achieved": flops / avg_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS,
+            "roofline": {"bound": "fp64-valu", "achieved": flops / avg_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / avg_launch_s / 1e12 / FP64_PEAK_TFLOPS,
-                         "traffic": traffic,
-                         "compute_unit": "FP64 VALU: the kernel issues no MFMA instructions; 'mfma' names the "
-                                         "compute roof, and MI355X's FP64 vector and FP64 matrix peaks are the "
-                                         "same 78.6 TFLOP/s",
+                         "traffic": traffic, "traffic_source": traffic_source,
+                         "compute_unit": "FP64 VALU: the kernels issue no MFMA instructions (DESIGN.md 2, 'Why no "
+                                         "MFMA'); the peak is MI355X's FP64 rate, which is the same 78.6 TFLOP/s "
+                                         "for vector and matrix instructions",
                          "achieved_basis": "SURVEY 8(d) flop count of a dense condensed PDIP (24N^3 per Hessian, "
                                            "48N^3 per iteration), F(N, mean iters) x B / avg step time; this is an "
                                            "equivalent dense-QP rate, not executed work",
@@ -185,9 +196,10 @@ def main():
                          "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
         }
         if args.inflight > 1:
-            out["inflight"] = inflight(args.inflight, args.steps, wb, B, N, mo, X, U, dev, world)
-        if args.closed_loop:
-            out["closed_loop"] = closed_loop(args.config, args.closed_loop, N, local)
+            head = {k: v.cpu().numpy() for k, v in (("st", st), ("it", it), ("U", Uo))}
+            out["inflight"] = inflight(args.inflight, args.steps, wb, B, N, mo, X, U, dev, head)
+        if cl is not None:
+            out["closed_loop"] = cl
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
             out["cpu_reference"] = cpu_reference(wb, N, args.cpu_seconds)
@@ -196,12 +208,13 @@ def main():
         dist.destroy_process_group()
 
 
-def inflight(K, steps, wb, B, N, mo, X, U, dev, world):
+def inflight(K, steps, wb, B, N, mo, X, U, dev, head):
     """Serving leg (not the headline `value`): K independent batches of B solves in flight at once, one
     solver context and one HIP stream each, `steps` rounds of K submissions.  A single batch leaves SIMDs idle
     while its slowest interior-point instance finishes (tail bound); independent batches on
-    other streams fill them.  Every batch is complete and checked (its status/iteration telemetry must equal
-    the sequential batch's); rank 0 only, after the headline timing."""
+    other streams fill them.  Every batch solves the headline inputs, and after the timed rounds each
+    context's last outputs (U, status, iterations) must equal the headline run's bit for bit, or this raises;
+    rank 0 only, after the headline timing."""
     import numpy as np
     import torch
     import mpcqp
@@ -234,88 +247,110 @@ def inflight(K, steps, wb, B, N, mo, X, U, dev, world):
             submit(*c)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    st0, it0 = ctx[0][2]["st"].cpu().numpy(), ctx[0][2]["it"].cpu().numpy()
-    same = all(np.array_equal(c[2]["st"].cpu().numpy(), st0) and np.array_equal(c[2]["it"].cpu().numpy(), it0)
-               and torch.equal(c[2]["U"], ctx[0][2]["U"]) for c in ctx[1:])
+    for k, c in enumerate(ctx):
+        o = c[2]
+        if not (np.array_equal(o["st"].cpu().numpy(), head["st"]) and np.array_equal(o["it"].cpu().numpy(), head["it"])
+                and np.array_equal(o["U"].cpu().numpy(), head["U"])):
+            raise RuntimeError(f"inflight: context {k}'s outputs differ from the headline batch's")
+    same = True
     for c in ctx:
         c[0].close()
     return {"batches_in_flight": K, "value_per_gpu": K * steps * B / dt, "unit": "solves/s",
-            "ms_per_batch": dt * 1e3 / (K * steps), "batches": K * steps, "outputs_identical_across_streams": same,
+            "ms_per_batch": dt * 1e3 / (K * steps), "batches": K * steps, "outputs_identical_to_headline": same,
             "note": "secondary serving measurement on rank 0 (per GPU): independent batches of the same shape on "
                     "K streams; the headline value above is one batch at a time"}
 
 
-def closed_loop(config, B, N, device, sqp_iters=4):
-    """B egos through run_simulation on the device (trajectory_tracking.py:377-443): starts near the
-    reference start (s0 ~ U(0,2), v0 ~ U(0.5,2)), the config's FSM preset, until every ego
-    passed s_max - 1 or 3000 steps.  Reports ego-steps/s over the whole call (FSM + solve + plant)."""
+def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_egos=4):
+    """B egos per GPU through run_simulation on the device (trajectory_tracking.py:377-443, mpc_closed_loop):
+    starts near the reference start (s0 ~ U(0,2), v0 ~ U(0.5,2)) drawn for all world * B egos,
+    each rank running its contiguous shard with the config's FSM preset, until every ego passed s_max - 1
+    or max_steps.  Drop-in solver default (Gauss-Newton SQP to the reference NLP optimum).  The one
+    collective: a gather to rank 0 of every ego's check quantities and the FP32 histories of the first
+    hist_egos egos of each shard (shard.py); rank 0 applies the restated verdicts to every ego."""
     import numpy as np
+    import torch
+    import torch.distributed as dist
     import mpcqp
+    import shard
     import workloads as W
     import trajectory_tracking as TT
     cfg = W.CONFIGS[config]
     ld = W.loader(cfg["traj"])
+    total = world * B
     rng = np.random.default_rng(cfg["seed"])
-    s0 = rng.uniform(0.0, 2.0, B)
-    x_init = np.array([[s, 0.0, 0.0, ld.get_state(s)[3], v] for s, v in zip(s0, rng.uniform(0.5, 2.0, B))])
-    fsm = None
+    s0, v0 = rng.uniform(0.0, 2.0, total), rng.uniform(0.5, 2.0, total)
+    lo, hi = shard.shard_range(total, world, rank)
+    x_init = np.array([[s0[i], 0.0, 0.0, ld.get_state(s0[i])[3], v0[i]] for i in range(lo, hi)])
+    fsm_obj = None
     if cfg["obstacles"] in ("fsm2", "fsm3"):
-        fsm = TT.fsm_params(TT.ObstaclesFSM(True, True, preset="trajectory2" if cfg["obstacles"] == "fsm2"
-                                            else "trajectory3"))
-    # Gauss-Newton SQP with 4 re-linearisations: a single QP at the reference warm start can stop for
-    # good behind the slower FSM car at N >= 10 (DESIGN.md 5b); the reference's SLSQP is an NLP solver
-    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, sqp_iters=sqp_iters), device=device)
+        fsm_obj = TT.ObstaclesFSM(True, True, preset="trajectory2" if cfg["obstacles"] == "fsm2" else "trajectory3")
+    fsm = TT.fsm_params(fsm_obj)
+    p = mpcqp.default_params(N=N, sqp_iters=TT.SQP_ITERS)
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, p, device=device)
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
-    r = slv.closed_loop(x_init, fsm, max_steps=3000, s_max=ld.s_max)
+    r = slv.closed_loop(x_init, fsm, max_steps=max_steps, s_max=ld.s_max)
     dt = time.perf_counter() - t0
-    steps = int(r["n_steps"].sum())
+    slv.close()
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    tl_pos = fsm_obj.tl_pos if fsm_obj is not None else 0.0
+    q = shard.closed_loop_quantities(r, lo, fsm_obj is not None, fsm_obj is not None, tl_pos)
+    rows = -(-total // world)
+    payloads = shard.gather_closed_loop(shard.pack_closed_loop(q, r, rows, hist_egos, max_steps),
+                                        device=dev if world > 1 else None)
+    if rank != 0:
+        return None
+    rep = shard.closed_loop_report(payloads, rows, hist_egos, max_steps, tuple(p.u_min), tuple(p.u_max), ld.s_max)
     ms = r["step_ms"][np.isfinite(r["step_ms"])]
-    return {"egos": B, "ego_steps": steps, "loop_steps": int(r["n_steps"].max()), "seconds": dt,
-            "ego_steps_per_s": steps / dt, "p50_step_ms": float(np.median(ms)) if ms.size else None,
-            "finished": int((r["n_steps"] < 3000).sum()),
-            "status_counts": np.bincount(r["hist_status"][r["hist_status"] >= 0], minlength=4).tolist(),
-            "fsm": cfg["obstacles"], "sqp_iters": sqp_iters, "checks": "tools/debug_cl.py runs the restated "
-            "trajectory_tracking_check on sample egos"}
+    return {"egos": rep["egos"], "ranks": rep["ranks"], "ego_steps": rep["ego_steps"], "seconds": dt,
+            "ego_steps_per_s": rep["ego_steps"] / dt, "loop_steps_rank0": int(r["n_steps"].max()),
+            "p50_step_ms_rank0": float(np.median(ms)) if ms.size else None,
+            "finished": int((rep["quantities"][:, 1] < max_steps).sum()), "checks_passed": rep["checks_passed"],
+            "fsm": cfg["obstacles"], "sqp_iters": TT.SQP_ITERS, "sqp_tol": p.sqp_tol,
+            "gathered_histories": f"FP32 [{rep['hist'].shape[0]} egos x {max_steps} steps x {shard.HIST_COLS}]",
+            "note": "restated trajectory_tracking_check verdicts applied by rank 0 to the gathered per-ego check "
+                    "quantities; real-time check = each batched step's device time (the latency of every ego's "
+                    "answer)"}
 
 
-def cpu_baseline(wb, N, mo, budget_s):
-    """The oracle's C restatement (same QP, same PDIP), OpenMP over the host cores, on a bounded
-    sample of the same egos.  kind = 'port' (the reference itself never travels to the GPU box)."""
-    import numpy as np
-    import oracle as O
-    import workloads as W
-    ld = W.loader(wb["traj"])
-    orc = O.Oracle(ld.X_ref, ld.U_ref)
-    p = O.default_params(N=N, max_obs=mo)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    n = min(512, wb["x0"].shape[0])
-    sl = slice(0, n)
-    obs = None if wb["obs"] is None else wb["obs"][sl]
-    nob = None if wb["n_obs"] is None else wb["n_obs"][sl]
-    orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)        # warm
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)
-        done += n
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by the oracle's C PDIP "
-                      f"(oracle/mpc_oracle.c) with OpenMP"}
+def host_cores():
+    """Host CPUs as the GPU box shows them: physical cores (lscpu, unique core/socket pairs) of the whole
+    machine, and the CPUs this process may run on (its affinity mask: the box's share)."""
+    import subprocess
+    phys = None
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        phys = len({ln for ln in out.splitlines() if ln and not ln.startswith("#")})
+    except Exception:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    return {"physical_cores_lscpu": phys, "affinity_cpus": aff, "logical_cpus": os.cpu_count()}
 
 
 def cpu_reference(wb, N, budget_s):
-    """The reference's own per-step solve (trajectory_tracking.py:213-263: warm start + scipy SLSQP,
-    ftol 1e-3, maxiter 15, finite-difference gradients), restated bit-exactly in oracle/slsqp_port.py
-    and run one ego at a time per host process on a bounded sample of the same egos."""
+    """The reference's per-step solve path (trajectory_tracking.py:213-263: warm start + scipy SLSQP, ftol
+    1e-3, maxiter 15, finite-difference gradients), restated in oracle/slsqp_port.py and run one ego at a
+    time per host process on a bounded sample of the same egos.  The restatement evaluates the reference
+    signal with numpy interpolation instead of scipy interp1d objects, so it runs faster per core than the
+    reference itself (SURVEY 6 measures the reference); it reaches the same iterates (tests/test_slsqp_port)."""
     import slsqp_port as SP
-    procs = min(16, os.cpu_count() or 1)
+    procs = min(16, host_cores()["affinity_cpus"])
     n = min(256, wb["x0"].shape[0])
     sl = slice(0, n)
     done, dt = SP.time_batch(wb["traj"], N, wb["x0"][sl], None if wb["obs"] is None else wb["obs"][sl],
                              None if wb["n_obs"] is None else wb["n_obs"][sl], budget_s=budget_s, procs=procs)
     return {"value": done / dt, "unit": "solves/s", "cores": procs, "kind": "port",
-            "sample": f"{done} solves of the first {n} egos of the same batch in {dt:.1f} s by the reference's "
-                      f"SLSQP solve path (oracle/slsqp_port.py, pinned to the reference's solve() outputs), "
+            "label": "restated SLSQP path with numpy interpolation (faster than the reference's scipy interp1d)",
+            "sample": f"{done} solves of the first {n} egos of the same batch in {dt:.1f} s by the restated SLSQP "
+                      f"solve path (oracle/slsqp_port.py, pinned to the reference's solve() outputs), "
                       f"{procs} processes"}
 
 

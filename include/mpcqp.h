@@ -103,9 +103,12 @@ int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, cons
  * Same argument contract as mpc_solve_batch (n_obs NULL = all max_obs rows; obs with max_obs == 0 is
  * MPC_E_ARG).  No host synchronisation, no allocation (graph-capturable): the two-phase work list is
  * allocated by mpc_create for up to 2^20 instances; a larger B runs the single-kernel path (same
- * results).  The work list belongs to the context: consecutive calls on one context are ordered on
- * the device even when they use different streams (a call on a new stream waits for the previous
- * call's kernels), so results never depend on the streams chosen. */
+ * results).  The work list belongs to the context: consecutive eager calls on one context are ordered
+ * on the device even when they use different streams (a call on a new stream waits for the previous
+ * call's kernels), so their results never depend on the streams chosen.  A call made while `stream` is
+ * being captured into a HIP graph records no such ordering (it would tie the graph to work outside
+ * it): replays of that graph must not overlap eager calls, or replays of another graph, on the same
+ * context -- run them on one stream, synchronise between them, or give the graph its own context. */
 int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const double* obs, const int* n_obs,
                            const double* ubar, double* u0, double* U, double* Xpred, int* status,
                            int* iters, void* stream);

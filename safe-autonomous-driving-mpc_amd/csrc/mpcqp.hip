@@ -1133,8 +1133,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 
     const int nsqp = Pr.sqp_iters < 0 ? 0 : Pr.sqp_iters;   // 0: return ubar and predict(x0, ubar)
     int status = MPC_OK, total_it = 0;
-    bool xo_ok = false;
-    double cstr[6] = {0, 0, 0, 0, 0, 0};   // LITE: cost data of stage k (this lane's only)              // MODE_XO: the crossover certified this instance
+    bool xo_ok = false;                    // MODE_XO: the crossover certified this instance
+    double cstr[6] = {0, 0, 0, 0, 0, 0};   // LITE: cost data of stage k (this lane's only)
     for (int sqp = 0; sqp < nsqp; ++sqp) {
         // ---- K1: nominal rollout == predict(x0, ubar), into Xr ------------------------------
         predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
@@ -2189,9 +2189,17 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     const bool split = kp.polish >= 2 && kp.sqp_iters == 1 && c->two_phase && G >= 2 && (size_t)B <= c->cap_wl;
     int* wl = split ? c->wl + 1 : nullptr;
     int* wcnt = split ? c->wl : nullptr;
+    // Under stream capture (a HIP graph being recorded) the cross-call ordering below is left out: waiting
+    // on wl_done, recorded outside the capture, would be a cross-capture dependency that invalidates the
+    // capture, and an event recorded inside it belongs to the graph.  Replays of a captured graph are
+    // therefore ordered against eager calls on the same context only by the caller (include/mpcqp.h).
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (split) HIPCHK(hipStreamIsCapturing(st, &cap), MPC_E_DEVICE);
+    const bool capturing = cap != hipStreamCaptureStatusNone;
     if (split) {
         // the previous split launch may still be reading the list on another stream: order after it
-        if (c->wl_pending && c->wl_stream != st) HIPCHK(hipStreamWaitEvent(st, c->wl_done, 0), MPC_E_DEVICE);
+        if (!capturing && c->wl_pending && c->wl_stream != st)
+            HIPCHK(hipStreamWaitEvent(st, c->wl_done, 0), MPC_E_DEVICE);
         // reset by a memset on the stream (not by the kernels): a captured graph replays correctly
         HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
     }
@@ -2214,9 +2222,11 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
         MPC_LAUNCH_GL(MODE_IPM);
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
-        HIPCHK(hipEventRecord(c->wl_done, st), MPC_E_DEVICE);
-        c->wl_stream = st;
-        c->wl_pending = true;
+        if (!capturing) {
+            HIPCHK(hipEventRecord(c->wl_done, st), MPC_E_DEVICE);
+            c->wl_stream = st;
+            c->wl_pending = true;
+        }
     } else {
         MPC_LAUNCH_GL(MODE_FULL);
     }
@@ -2358,23 +2368,39 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
         return fail(MPC_E_ALLOC, "hipMalloc closed-loop histories");
     }
     hipStream_t st = c->stream;
-    // steps that never run stay NaN / -1 (all-ones bytes)
-    if (d_hx) hipMemsetAsync(d_hx, 0xff, nb * (ns + 1) * 5 * 8, st);
-    if (d_hu) hipMemsetAsync(d_hu, 0xff, nb * ns * 2 * 8, st);
-    if (d_ho) hipMemsetAsync(d_ho, 0xff, nb * ns * 8, st);
-    if (d_ht) hipMemsetAsync(d_ht, 0xff, nb * ns * 4, st);
-    if (d_hs) hipMemsetAsync(d_hs, 0xff, nb * ns * 4, st);
-    if (hipMemcpyAsync(d_xinit, x_init, nb * 5 * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
+    std::vector<hipEvent_t> ev;
+    auto cleanup = [&]() {
+        hipStreamSynchronize(st);
+        for (auto& e : ev)
+            if (e) hipEventDestroy(e);
         release();
-        return fail(MPC_E_DEVICE, "hipMemcpy x_init");
+    };
+    // steps that never run stay NaN / -1 (all-ones bytes)
+    bool ok0 = true;
+    if (d_hx) ok0 = ok0 && hipMemsetAsync(d_hx, 0xff, nb * (ns + 1) * 5 * 8, st) == hipSuccess;
+    if (d_hu) ok0 = ok0 && hipMemsetAsync(d_hu, 0xff, nb * ns * 2 * 8, st) == hipSuccess;
+    if (d_ho) ok0 = ok0 && hipMemsetAsync(d_ho, 0xff, nb * ns * 8, st) == hipSuccess;
+    if (d_ht) ok0 = ok0 && hipMemsetAsync(d_ht, 0xff, nb * ns * 4, st) == hipSuccess;
+    if (d_hs) ok0 = ok0 && hipMemsetAsync(d_hs, 0xff, nb * ns * 4, st) == hipSuccess;
+    ok0 = ok0 && hipMemcpyAsync(d_xinit, x_init, nb * 5 * 8, hipMemcpyHostToDevice, st) == hipSuccess;
+    if (!ok0) {
+        cleanup();
+        return fail(MPC_E_DEVICE, "closed-loop buffer initialisation");
     }
     const dim3 tb(256), tg((B + 255) / 256);
     hipLaunchKernelGGL(cl_init_kernel, tg, tb, 0, st, B, F, C, d_xinit, s_stop, d_hx, d_ns, max_steps);
-    std::vector<hipEvent_t> ev;
     if (step_ms) {
-        ev.resize(ns + 1);
-        for (auto& e : ev) hipEventCreate(&e);
-        hipEventRecord(ev[0], st);
+        ev.assign(ns + 1, nullptr);
+        for (auto& e : ev)
+            if (hipEventCreate(&e) != hipSuccess) {
+                e = nullptr;
+                cleanup();
+                return fail(MPC_E_DEVICE, "hipEventCreate (step timing)");
+            }
+        if (hipEventRecord(ev[0], st) != hipSuccess) {
+            cleanup();
+            return fail(MPC_E_DEVICE, "hipEventRecord (step timing)");
+        }
     }
     int steps_run = 0;
     rc = MPC_SUCCESS;
@@ -2384,10 +2410,16 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
         rc = launch_solve(c, kp, B, C.x, with_fsm ? C.obs : nullptr, with_fsm ? C.nobs : nullptr, nullptr, C.u0,
                           nullptr, nullptr, C.status, nullptr, st);
         if (rc) break;
-        hipMemsetAsync(C.n_active, 0, 4, st);
+        if (hipMemsetAsync(C.n_active, 0, 4, st) != hipSuccess) {
+            rc = fail(MPC_E_DEVICE, "closed-loop active-count reset");
+            break;
+        }
         hipLaunchKernelGGL(cl_plant_kernel, tg, tb, 0, st, c->tab, B, kp.dt, C, s_stop, d_hx, d_hu, d_hs, d_ns, step,
                            max_steps);
-        if (step_ms) hipEventRecord(ev[step + 1], st);
+        if (step_ms && hipEventRecord(ev[step + 1], st) != hipSuccess) {
+            rc = fail(MPC_E_DEVICE, "hipEventRecord (step timing)");
+            break;
+        }
         steps_run = step + 1;
         if ((step & 7) == 7 || step == max_steps - 1) {     // every 8 steps: has every ego left the loop?
             int na = 0;
@@ -2413,13 +2445,11 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
     if (step_ms) {
         for (size_t i = 0; i < ns; ++i) {
             float ms = NAN;
-            if ((int)i < steps_run) hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+            if ((int)i < steps_run && hipEventElapsedTime(&ms, ev[i], ev[i + 1]) != hipSuccess) ms = NAN;
             step_ms[i] = ms;
         }
-        for (auto& e : ev) hipEventDestroy(e);
     }
-    hipStreamSynchronize(st);
-    release();
+    cleanup();
     return rc;
 }
 

@@ -13,39 +13,52 @@ CPU_LIMIT = 150      # ms
 SAFETY_DIST = 1.0
 
 
-def check_summary(u_min, u_max, hist_x, hist_u, hist_t, hist_obs_s, hist_tl_red, dynamic_obstacle,
-                  traffic_light, tl_pos, s_total):
-    """All checks of sanity_checks.py:79-184 as a dict of bools (+ the measured quantities)."""
+def check_quantities(hist_x, hist_u, hist_t, hist_obs_s, hist_tl_red, dynamic_obstacle, traffic_light, tl_pos):
+    """What sanity_checks.py:79-184 measures over one closed-loop run (the inputs of the verdicts):
+    final s, max |d|, control extremes, max solve time, min gap to the dynamic obstacle (NaN if it never
+    existed) and whether the ego crossed tl_pos while the light was RED.  Per ego, on the rank that ran it."""
     hist_x = np.asarray(hist_x, np.float64)
-    hist_u = np.asarray(hist_u, np.float64)
+    hist_u = np.asarray(hist_u, np.float64).reshape(-1, 2)
     hist_t = np.asarray(hist_t, np.float64)
-    out = {}
-    out["s_final"] = float(hist_x[-1, 0])
-    out["destination"] = not (out["s_final"] < s_total - 1.0)                          # :97-103
-    out["max_dev"] = float(np.max(np.abs(hist_x[:, 1])))
-    out["on_road"] = not (out["max_dev"] > LATERAL_LIMIT)                              # :105-111
-    u1, u2 = hist_u[:, 0], hist_u[:, 1]
-    out["steer_ok"] = not ((np.min(u1) < u_min[0] - CONTROLS_TOL) or (np.max(u1) > u_max[0] + CONTROLS_TOL))
-    out["accel_ok"] = not ((np.min(u2) < u_min[1] - CONTROLS_TOL) or (np.max(u2) > u_max[1] + CONTROLS_TOL))
-    out["max_cpu_ms"] = float(np.max(hist_t) * 1000) if hist_t.size else 0.0
-    out["realtime"] = not (out["max_cpu_ms"] > CPU_LIMIT)                             # :133-139
-    out["obstacle_ok"] = True
-    out["min_obs_dist"] = float("nan")
+    q = {"s_final": float(hist_x[-1, 0]), "max_dev": float(np.max(np.abs(hist_x[:, 1])))}
+    q["u1_min"], q["u1_max"] = float(np.min(hist_u[:, 0])), float(np.max(hist_u[:, 0]))
+    q["u2_min"], q["u2_max"] = float(np.min(hist_u[:, 1])), float(np.max(hist_u[:, 1]))
+    q["max_cpu_ms"] = float(np.max(hist_t) * 1000) if hist_t.size else 0.0
+    q["min_obs_dist"] = float("nan")
     if dynamic_obstacle:                                                              # :141-161
         obs_s = np.asarray(hist_obs_s, np.float64)
         valid = ~np.isnan(obs_s)
         if np.any(valid):
             m = min(len(hist_x), len(obs_s))
-            d = obs_s[:m][valid[:m]] - hist_x[:m, 0][valid[:m]]
-            out["min_obs_dist"] = float(np.min(d))
-            out["obstacle_ok"] = not (out["min_obs_dist"] < SAFETY_DIST)
-    out["light_ok"] = True
+            q["min_obs_dist"] = float(np.min(obs_s[:m][valid[:m]] - hist_x[:m, 0][valid[:m]]))
+    q["red_pass"] = 0.0
     if traffic_light:                                                                 # :163-181
         idx = np.where(hist_x[:, 0] > tl_pos)[0]
         if len(idx) > 0 and idx[0] < len(hist_tl_red) and bool(hist_tl_red[idx[0]]):
-            out["light_ok"] = False
-    out["passed"] = all(out[k] for k in ("destination", "on_road", "steer_ok", "accel_ok", "realtime",
-                                         "obstacle_ok", "light_ok"))
+            q["red_pass"] = 1.0
+    return q
+
+
+def check_verdicts(q, u_min, u_max, s_total):
+    """The verdicts of sanity_checks.py:79-184 from check_quantities' measurements (a dict, or any mapping
+    with the same keys: rank 0 applies this to the gathered per-ego summaries of every rank)."""
+    v = {"destination": not (q["s_final"] < s_total - 1.0),                            # :97-103
+         "on_road": not (q["max_dev"] > LATERAL_LIMIT),                                # :105-111
+         "steer_ok": not ((q["u1_min"] < u_min[0] - CONTROLS_TOL) or (q["u1_max"] > u_max[0] + CONTROLS_TOL)),
+         "accel_ok": not ((q["u2_min"] < u_min[1] - CONTROLS_TOL) or (q["u2_max"] > u_max[1] + CONTROLS_TOL)),
+         "realtime": not (q["max_cpu_ms"] > CPU_LIMIT),                                # :133-139
+         "obstacle_ok": bool(np.isnan(q["min_obs_dist"]) or not (q["min_obs_dist"] < SAFETY_DIST)),
+         "light_ok": not q["red_pass"]}
+    v["passed"] = all(v.values())
+    return v
+
+
+def check_summary(u_min, u_max, hist_x, hist_u, hist_t, hist_obs_s, hist_tl_red, dynamic_obstacle,
+                  traffic_light, tl_pos, s_total):
+    """All checks of sanity_checks.py:79-184 as a dict of bools (+ the measured quantities)."""
+    q = check_quantities(hist_x, hist_u, hist_t, hist_obs_s, hist_tl_red, dynamic_obstacle, traffic_light, tl_pos)
+    out = dict(q)
+    out.update(check_verdicts(q, u_min, u_max, s_total))
     return out
 
 

@@ -48,3 +48,90 @@ def reduce_telemetry(mat):
     return {"status_counts": {k: int(mat[:, i].sum()) for i, k in enumerate(TELEMETRY_FIELDS[:4])},
             "mean_iters": float(mat[:, 4].sum() / max(n, 1.0)), "max_iters": int(mat[:, 5].max()),
             "egos": int(n), "ranks": int(mat.shape[0])}
+
+
+# ---------------------------------------------------------------------------------------------
+# closed-loop telemetry (SURVEY 8(e)): each rank runs mpc_closed_loop on its ego shard; one gather
+# brings every ego's check quantities, plus the FP32 histories of the first `hist_egos` egos of each
+# shard, to rank 0, which applies the restated verdicts (sanity_checks.check_verdicts) to all egos.
+# ---------------------------------------------------------------------------------------------
+CL_FIELDS = ("ego", "n_steps", "s_final", "max_dev", "u1_min", "u1_max", "u2_min", "u2_max", "max_cpu_ms",
+             "min_obs_dist", "red_pass")
+HIST_COLS = 7          # s, d, o, k, v of the state after the step, then u1, u2 of the step
+
+
+def closed_loop_quantities(r, lo, dynamic_obstacle, traffic_light, tl_pos, step_ms=None):
+    """[B, len(CL_FIELDS)] float64 check quantities of a closed_loop() result (mpcqp.Solver.closed_loop
+    layout) for egos lo .. lo + B - 1.  The solve time each ego saw at a step is that batched step's
+    device time (step_ms), the latency of its answer."""
+    from sanity_checks import check_quantities
+    ns = np.asarray(r["n_steps"])
+    B = ns.size
+    sm = np.asarray(r["step_ms"] if step_ms is None else step_ms, np.float64)
+    out = np.zeros((B, len(CL_FIELDS)))
+    for b in range(B):
+        n = int(ns[b])
+        if n == 0:
+            out[b] = [lo + b, 0, r["hist_x"][b, 0, 0], abs(r["hist_x"][b, 0, 1])] + [0.0] * 4 + [0.0, np.nan, 0.0]
+            continue
+        q = check_quantities(r["hist_x"][b, :n + 1], r["hist_u"][b, :n], sm[:n] / 1e3, r["hist_obs_s"][b, :n],
+                             np.asarray(r["hist_tl"][b, :n]) == 0, dynamic_obstacle, traffic_light, tl_pos)
+        out[b] = [lo + b, n] + [q[k] for k in CL_FIELDS[2:]]
+    return out
+
+
+def pack_closed_loop(quant, r, rows, hist_egos, max_steps):
+    """One rank's gather payload (bytes, the same size on every rank): int32 header (egos, history egos),
+    float64 quantities padded to `rows` egos, float32 histories [hist_egos, max_steps, HIST_COLS] (NaN past
+    an ego's last step)."""
+    B = quant.shape[0]
+    h = min(hist_egos, B)
+    q = np.full((rows, len(CL_FIELDS)), np.nan)
+    q[:B] = quant
+    hist = np.full((hist_egos, max_steps, HIST_COLS), np.nan, np.float32)
+    if h:
+        hist[:h, :, :5] = r["hist_x"][:h, 1:max_steps + 1]
+        hist[:h, :, 5:] = r["hist_u"][:h, :max_steps]
+    return np.concatenate([np.array([B, h], np.int32).view(np.uint8), q.view(np.uint8).ravel(),
+                           hist.view(np.uint8).ravel()])
+
+
+def unpack_closed_loop(buf, rows, hist_egos, max_steps):
+    buf = np.ascontiguousarray(buf, np.uint8)
+    B, h = buf[:8].view(np.int32)
+    nq = rows * len(CL_FIELDS) * 8
+    q = buf[8:8 + nq].view(np.float64).reshape(rows, len(CL_FIELDS))[:B]
+    hist = buf[8 + nq:].view(np.float32).reshape(hist_egos, max_steps, HIST_COLS)[:h]
+    return q, hist
+
+
+def gather_closed_loop(payload, device=None):
+    """The one collective of the closed loop: gather of every rank's payload to rank 0 (RCCL with the
+    "nccl" backend, gloo on CPU).  Returns the list of payloads on rank 0 and None elsewhere; without a
+    process group, [payload]."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [payload]
+    t = torch.as_tensor(payload, device=device)
+    if dist.get_rank() == 0:
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.gather(t, gather_list=out, dst=0)
+        return [o.cpu().numpy() for o in out]
+    dist.gather(t, dst=0)
+    return None
+
+
+def closed_loop_report(payloads, rows, hist_egos, max_steps, u_min, u_max, s_total):
+    """Rank 0: the restated verdicts over every ego of every rank, and the gathered histories."""
+    from sanity_checks import check_verdicts
+    qs, hists = zip(*(unpack_closed_loop(p, rows, hist_egos, max_steps) for p in payloads))
+    q = np.concatenate(qs)
+    names = ("destination", "on_road", "steer_ok", "accel_ok", "realtime", "obstacle_ok", "light_ok", "passed")
+    counts = dict.fromkeys(names, 0)
+    for row in q:
+        v = check_verdicts(dict(zip(CL_FIELDS, row)), u_min, u_max, s_total)
+        for k in names:
+            counts[k] += int(v[k])
+    return {"egos": int(q.shape[0]), "ranks": len(payloads), "ego_steps": int(q[:, 1].sum()),
+            "checks_passed": counts, "quantities": q, "hist": np.concatenate(hists)}

@@ -4,9 +4,11 @@ Generator: numpy default_rng(seed) (PCG64).  Per ego (single-step microbench):
   s0 ~ U(0, 0.8 s_max); d0 = d_ref(s0) + N(0, 0.05); o0 = o_ref(s0) + N(0, 0.01);
   k0 = k_ref(s0); v0 = max(0.5, v_ref(s0) + N(0, 0.5)).
 Obstacle slabs:
-  'fsm2' / 'fsm3'  snapshot of an ObstaclesFSM (trajectory_tracking.py:292-327 presets): the dynamic
-                   car (v = 4 m/s) ahead of the ego w.p. 0.5 at s0 + U(8, 70); the RED light at tl_pos
-                   when 0 < tl_pos - s0 < tl_trigger_s.  max_obs = 2.
+  'fsm2' / 'fsm3'  snapshot of an ObstaclesFSM with the geometry of its preset (trajectory_tracking.py:
+                   292-308 for trajectory2, :311-327 for trajectory3): the dynamic car (v = 4 m/s) exists
+                   only once the ego has passed obs_trigger_s and until the car passes obs_end_s (:339-350);
+                   it drives ahead of the ego (the ego cannot overtake it), at max(obs_start_s, s0 + U(8, 70));
+                   the RED light at tl_pos when 0 < tl_pos - s0 < tl_trigger_s (:357-361).  max_obs = 2.
   'const8'         8 constant-velocity cars: s_i = s0 + 25 + 50 i + U(0, 10), v_i ~ U(2, 10).
 """
 import numpy as np
@@ -22,7 +24,8 @@ CONFIGS = {
     "C5": dict(traj=3, N=40, B=65536, seed=5, obstacles="const8", gpus=8),
 }
 
-_FSM = {"fsm2": dict(tl_pos=550.0, tl_trigger_s=100.0), "fsm3": dict(tl_pos=2000.0, tl_trigger_s=100.0)}
+_FSM = {"fsm2": dict(obs_trigger_s=710.0, obs_start_s=780.0, obs_end_s=1050.0, tl_pos=550.0, tl_trigger_s=100.0),
+        "fsm3": dict(obs_trigger_s=5.0, obs_start_s=150.0, obs_end_s=850.0, tl_pos=2000.0, tl_trigger_s=100.0)}
 
 _LOADERS = {}
 
@@ -58,7 +61,6 @@ def make_batch(name, B=None, seed=None, offset=0):
     max_obs = 0
     if kind in _FSM:
         max_obs = 2
-        pc = rs[4].uniform(size=tot)
         pd = rs[5].uniform(8.0, 70.0, tot)
         obs = np.zeros((B, 2, 2))
         n_obs = np.zeros(B, np.int32)
@@ -66,8 +68,9 @@ def make_batch(name, B=None, seed=None, offset=0):
         for b in range(B):
             i = offset + b
             n = 0
-            if pc[i] < 0.5:
-                obs[b, n] = (x0[b, 0] + pd[i], 4.0)
+            car = max(f["obs_start_s"], x0[b, 0] + pd[i])
+            if x0[b, 0] >= f["obs_trigger_s"] and car <= f["obs_end_s"]:
+                obs[b, n] = (car, 4.0)
                 n += 1
             if 0.0 < f["tl_pos"] - x0[b, 0] < f["tl_trigger_s"]:
                 obs[b, n] = (f["tl_pos"], 0.0)

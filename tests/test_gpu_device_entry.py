@@ -142,3 +142,41 @@ def test_obstacles_with_max_obs_zero_are_refused(lib):
     obs = np.ascontiguousarray(wb["obs"])
     rc = lib.lib().mpc_solve_batch(slv.h, B, lib._p(x0), lib._p(obs), None, None, None, None, None, None, None)
     assert rc == -1 and "max_obs" in lib.last_error()
+
+
+def test_graph_capture_on_side_stream_after_eager_warmup(lib):
+    """Eager warm-up call on the current stream, then the same call captured into a HIP graph on a side
+    stream (torch.cuda.graph's pattern) and replayed: the capture must succeed (no wait on an event
+    recorded outside it) and every replay must equal the eager result, including after new inputs are
+    copied into the captured buffers."""
+    torch = pytest.importorskip("torch")
+    import workloads as W
+    wa = W.make_batch("C3", B=2048, seed=31)
+    wb = W.make_batch("C3", B=2048, seed=32)
+    slv = make_solver(lib, wa["traj"], wa["N"], wa["max_obs"])
+    ra = slv.solve_batch(wa["x0"], wa["obs"], wa["n_obs"])
+    rb = slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
+    out, keep = device_solve(slv, wa, torch)                  # eager warm-up (records the ordering event)
+    assert_identical(to_host(out, torch), ra, "eager")
+    x0, obs, nob = keep
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    ptr = lambda x: 0 if x is None else x.data_ptr()
+    with torch.cuda.graph(g, stream=side):
+        slv.solve_batch_device(2048, ptr(x0), ptr(obs), ptr(nob), 0, ptr(out["u0"]), ptr(out["U"]),
+                               ptr(out["Xpred"]), ptr(out["status"]), ptr(out["iters"]),
+                               stream=torch.cuda.current_stream().cuda_stream)
+    for _ in range(2):
+        for k in out:
+            out[k].zero_()
+        g.replay()
+        assert_identical(to_host(out, torch), ra, "replay")
+    x0.copy_(torch.as_tensor(wb["x0"]))
+    obs.copy_(torch.as_tensor(wb["obs"]))
+    nob.copy_(torch.as_tensor(wb["n_obs"]))
+    g.replay()
+    assert_identical(to_host(out, torch), rb, "replay on new inputs")
+    # an eager call after the replays (same stream) still orders correctly
+    o2, _ = device_solve(slv, wa, torch)
+    assert_identical(to_host(o2, torch), ra, "eager after graph")

@@ -33,32 +33,47 @@ def tt():
 
 
 def test_gpu_sqp_reaches_reference_nlp_optimum(tt):
+    """Same contract as tests/test_nlp_golden.py::test_oracle_sqp_reaches_reference_nlp_optimum, on the GPU
+    through the drop-in surface: the golden optimum to TOL_NLP_MEAS, or (at most MAX_OTHER_OPTIMA cases) a
+    different converged, feasible local optimum of the non-convex reference problem."""
+    import oracle as O
+    from conftest import traj_arrays
+    from test_nlp_golden import MAX_OTHER_OPTIMA, classify
     TT, TL, bt = tt
     cases, _ = golden_cases("nlp_golden")
     trackers = {i: TT.TrajectoryTracker(TL(bt(i))) for i in (1, 2, 3)}
-    worst, n = 0.0, 0
+    orcs = {i: O.Oracle(*traj_arrays(i)) for i in (1, 2, 3)}
+    worst, n, other = 0.0, 0, []
     for j, c in enumerate(cases):
         if not bool(c["certified"]):
             continue
         mpc = trackers[int(c["traj"])]
         mpc.N = int(c["N"])
         obs = [{"s": s, "v": v, "type": "car"} for s, v in c["obs"]]
-        errs = []
-        for K in (1, 2, 3, 4, TT.SQP_ITERS):
+        errs, Us = [], []
+        for K in (1, 2, 3, 4, TT.SQP_ITERS, TT.SQP_ITERS + 20):
             mpc.sqp_iters = K
             r = mpc.solve_batch(c["x0"][None], [obs])
             errs.append(float(np.abs(r["U"][0].ravel() - c["U_nlp"]).max()))
+            Us.append((r["U"][0].copy(), int(r["status"][0])))
         mpc.sqp_iters = TT.SQP_ITERS
         u0, pred_X, _ = mpc.solve(c["x0"], obs)           # the drop-in surface, same answer
-        assert np.array_equal(u0, r["U"][0, 0])
-        print(f"case {j} traj{int(c['traj'])} N={int(c['N'])} obs={len(obs)} |U-U_nlp| K=1,2,3,4,cap: "
-              + " ".join(f"{e:.1e}" for e in errs))
-        assert errs[-1] <= TOL_NLP and errs[-1] <= TOL_NLP_MEAS, (j, errs)
-        assert int(r["status"][0]) == 0
-        worst = max(worst, errs[-1])
+        assert np.array_equal(u0, Us[-2][0][0])
+        p = O.default_params(N=mpc.N, max_obs=len(obs))
+        o = c["obs"] if len(obs) else None
+        kind, e = classify(Us[-2][0], Us[-1][0], c,
+                           lambda U: orcs[int(c["traj"])].constraints(p, c["x0"], o, U.ravel()).min())
+        print(f"case {j} traj{int(c['traj'])} N={mpc.N} obs={len(obs)} {kind} |U-U_nlp| K=1,2,3,4,cap: "
+              + " ".join(f"{x:.1e}" for x in errs[:-1]))
+        assert kind != "bad", (j, errs)
+        if kind == "nlp":
+            assert e <= TOL_NLP and e <= TOL_NLP_MEAS and Us[-2][1] == 0, (j, errs)
+            worst = max(worst, e)
+        else:
+            other.append(j)
         n += 1
-    assert n >= 45
-    print(f"GPU SQP: worst |U - U_nlp| over {n} certified cases = {worst:.2e}")
+    assert n >= 45 and len(other) <= MAX_OTHER_OPTIMA
+    print(f"GPU SQP: worst |U - U_nlp| over {n - len(other)} certified cases = {worst:.2e}; other local optima {other}")
 
 
 def _replay_fsm(TT, fsm, hx, n):

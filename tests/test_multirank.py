@@ -81,3 +81,98 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
     assert tel["status_counts"]["ok"] == int((ref["status"] == 0).sum())
     assert tel["max_iters"] == int(ref["iters"].max())
     assert tel["mean_iters"] == pytest.approx(float(ref["iters"].mean()))
+
+
+# ---------------------------------------------------------------------------------------------
+# closed-loop telemetry: sharded closed loops + one gather of per-ego check quantities and FP32 histories
+# ---------------------------------------------------------------------------------------------
+CL_TOTAL, CL_STEPS, CL_HIST = 6, 260, 2
+
+
+def cl_inputs(total):
+    """Starts near the traffic light and the car trigger of the trajectory2 preset, so both scenarios run."""
+    rng = np.random.default_rng(17)
+    s0 = np.where(np.arange(total) % 2 == 0, rng.uniform(440.0, 460.0, total), rng.uniform(690.0, 700.0, total))
+    return np.column_stack([s0, rng.normal(0, 0.03, total), np.zeros(total), np.zeros(total),
+                            rng.uniform(7.0, 9.0, total)])
+
+
+def cpu_closed_loop(x_init, max_steps, N=5):
+    """CPU stand-in for mpcqp.Solver.closed_loop (same result layout): the shim's FSM and plant with the
+    oracle's solve; every step is charged 1 ms (deterministic quantities)."""
+    import oracle as O
+    import trajectory_tracking as TT
+    from trajectory_loader import TrajectoryLoader, builtin_trajectory
+    traj = TrajectoryLoader(builtin_trajectory(2))
+    orc = O.Oracle(traj.X_ref, traj.U_ref)
+    B = x_init.shape[0]
+    r = dict(hist_x=np.full((B, max_steps + 1, 5), np.nan), hist_u=np.full((B, max_steps, 2), np.nan),
+             hist_obs_s=np.full((B, max_steps), np.nan), hist_tl=np.full((B, max_steps), -1, np.int32),
+             n_steps=np.zeros(B, np.int32), step_ms=np.ones(max_steps))
+    mpc = TT.TrajectoryTracker(traj)
+    for b in range(B):
+        fsm = TT.ObstaclesFSM(True, True)
+        x = x_init[b].copy()
+        r["hist_x"][b, 0] = x
+        n = 0
+        while x[0] <= traj.s_max - 1.0 and n < max_steps:
+            obstacles, tl = fsm.update(0.2, x[0], x[4])
+            ob = np.array([[o["s"], o["v"]] for o in obstacles]).reshape(-1, 2)
+            res = orc.solve(O.default_params(N=N, max_obs=len(ob), sqp_iters=TT.SQP_ITERS), x, ob if len(ob) else None)
+            x = x + 0.2 * mpc.dynamics(x, res["u0"], traj.get_state(x[0])[3])
+            r["hist_x"][b, n + 1] = x
+            r["hist_u"][b, n] = res["u0"]
+            car = [o["s"] for o in obstacles if o["type"] == "car"]
+            r["hist_obs_s"][b, n] = car[0] if car else np.nan
+            r["hist_tl"][b, n] = 1 if tl == "GREEN" else 0
+            n += 1
+        r["n_steps"][b] = n
+    return r, traj
+
+
+def _cl_rank_main(rank, world, port, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [here, root, os.path.join(root, "safe-autonomous-driving-mpc_amd"), os.path.join(root, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import shard
+    from test_multirank import cl_inputs, cpu_closed_loop, CL_TOTAL, CL_STEPS, CL_HIST
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard.shard_range(CL_TOTAL, world, rank)
+    r, traj = cpu_closed_loop(cl_inputs(CL_TOTAL)[lo:hi], CL_STEPS)
+    q = shard.closed_loop_quantities(r, lo, True, True, 550.0)
+    rows = -(-CL_TOTAL // world)
+    payloads = shard.gather_closed_loop(shard.pack_closed_loop(q, r, rows, CL_HIST, CL_STEPS))
+    if rank == 0:
+        rep = shard.closed_loop_report(payloads, rows, CL_HIST, CL_STEPS, (-0.6, -5.0), (0.6, 4.0), traj.s_max)
+        np.savez(os.path.join(outdir, "cl_report.npz"), q=rep["quantities"], hist=rep["hist"],
+                 passed=rep["checks_passed"]["passed"], ranks=rep["ranks"])
+    else:
+        assert payloads is None
+    dist.destroy_process_group()
+
+
+def test_two_rank_closed_loop_gather_matches_single_process(tmp_path):
+    """Each rank runs the closed loop of its ego shard; rank 0 gathers (one collective) every ego's check
+    quantities and the FP32 histories of the first CL_HIST egos of each shard, and applies the verdicts:
+    all of it equals the single-process run."""
+    import torch.multiprocessing as mp
+    import shard
+    from sanity_checks import check_verdicts
+    mp.spawn(_cl_rank_main, args=(WORLD, _free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    rep = np.load(tmp_path / "cl_report.npz")
+    r, traj = cpu_closed_loop(cl_inputs(CL_TOTAL), CL_STEPS)
+    q = shard.closed_loop_quantities(r, 0, True, True, 550.0)
+    assert int(rep["ranks"]) == WORLD
+    assert np.array_equal(rep["q"], q, equal_nan=True)
+    # histories: the first CL_HIST egos of each shard, in rank order
+    keep = [e for rk in range(WORLD) for e in range(*shard.shard_range(CL_TOTAL, WORLD, rk))[:CL_HIST]]
+    exp = np.concatenate([r["hist_x"][keep, 1:CL_STEPS + 1], r["hist_u"][keep, :CL_STEPS]], axis=2).astype(np.float32)
+    assert np.array_equal(rep["hist"], exp, equal_nan=True)
+    passed = sum(check_verdicts(dict(zip(shard.CL_FIELDS, row)), (-0.6, -5.0), (0.6, 4.0), traj.s_max)["passed"]
+                 for row in q)
+    assert int(rep["passed"]) == passed
+    # the scenarios ran: the light switched for the egos starting before it, the car appeared for the others
+    assert (r["hist_tl"][0::2] == 1).any(axis=1).all() and np.isfinite(r["hist_obs_s"][1::2]).any(axis=1).all()
