@@ -1,7 +1,7 @@
 # GPU test pass: the whole -m gpu suite in one process, every test time-limited, then a short bench.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -v -s --timeout 300 --timeout-method thread -rA \
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -v -s --timeout 300 --timeout-method thread -rA \
     > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed|^E " gpurun_out/gpu_tests.log | head -20
 [ $rc -eq 0 ] || exit $rc
