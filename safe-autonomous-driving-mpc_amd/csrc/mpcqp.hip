@@ -196,6 +196,9 @@ __host__ __device__ constexpr bool acl_on(int GL, int NT) { return NT > 0 || GL 
 #define DQ_ZC 8
 #define DQ_ZA 10
 
+// stage cache record of the split launch, per work-list slot: ub [N][2] then Xr [N+1][5]
+__host__ __device__ constexpr int stage_cache_doubles(int N) { return 2 * N + 5 * (N + 1); }
+
 __host__ __device__ inline int lds_doubles(int N, bool acl, bool lite = false) {
     int NP = N + 1;
     int n = (acl ? N * 30 : 0) + N * A5S + (lite ? 0 : NP * 6) + NP * QRS + N * 2 + N * KRS + N * SIS + NP * QHS + N * 2 +
@@ -1030,10 +1033,13 @@ __device__ __forceinline__ constexpr int rid(int j) { return OBS ? j : (j < 6 ? 
 // appends the others to a device work list; MODE_IPM then runs the interior point (and polish) on the
 // listed instances only.  Results are identical (a failed crossover leaves no state behind), but the
 // expensive instances all start at once instead of queueing behind cheap ones on the same SIMD
-// ("two-phase launch").
+// ("two-phase launch").  MODE_ONE is MODE_FULL for a single QP (sqp_iters = 1):
+// the SQP loop is then a compile-time single pass, so no state is carried across it (the runtime loop
+// costs the one-launch kernels ~400 B of scratch per lane at N = 40).
 #define MODE_FULL 0
 #define MODE_XO 1
 #define MODE_IPM 2
+#define MODE_ONE 3
 
 // NT > 0: kernel specialised for horizon N = NT (the stage recursions are unrolled); NT = 0: any N.
 template <int GL, bool OBS, int MODE, int NT>
@@ -1041,7 +1047,8 @@ __global__ void __launch_bounds__(WAVE, MODE == MODE_XO ? 2 : 1)   // crossover:
 mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g, const double* __restrict__ obsg,
                  const int* __restrict__ nobsg, const double* __restrict__ ubarg, double* __restrict__ u0g,
                  double* __restrict__ Ug, double* __restrict__ Xg, int* __restrict__ statusg,
-                 int* __restrict__ itersg, int* __restrict__ wlist, int* __restrict__ wcount) {
+                 int* __restrict__ itersg, int* __restrict__ wlist, int* __restrict__ wcount,
+                 double* __restrict__ stc) {
     constexpr int G = WAVE / GL;
     constexpr int NR = OBS ? NROW : NROW - 2;    // soft rows held per lane (6, 7: obstacle rows)
     // the Riccati solves are fully unrolled (compile-time horizon) in the obstacle-free kernels only:
@@ -1056,13 +1063,15 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     const int grp = ln / GL, gl = ln % GL;
     int b;
     bool bvalid;
+    int cslot = 0;      // MODE_IPM: work-list slot whose record this group uses (a spare group repeats the last)
     if (MODE == MODE_IPM) {
         // instances deferred by the MODE_XO launch; waves past the end of the list exit at once
         const int cnt = *wcount;
         if ((int)blockIdx.x * G >= cnt) return;
         const int slot = blockIdx.x * G + grp;
         bvalid = slot < cnt;
-        b = wlist[bvalid ? slot : cnt - 1];
+        cslot = bvalid ? slot : cnt - 1;
+        b = wlist[cslot];
     } else {
         b = blockIdx.x * G + grp;
         bvalid = b < B;
@@ -1103,8 +1112,20 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         row_coef(rid<OBS>(j), hL, Pr.L, Pr.tgap, cf[j]);
     }
 
+    // stage cache of the split launch (stc != nullptr): MODE_XO leaves each deferred instance's
+    // linearisation point ub [N][2] and nominal rollout Xr [N+1][5] at its work-list slot, so MODE_IPM
+    // loads them instead of repeating the warm start and the rollout (stage_cache_doubles)
+    const bool cached = MODE == MODE_IPM && stc != nullptr;
+    const double* stc_in = nullptr;
+    if (cached) stc_in = stc + (size_t)cslot * stage_cache_doubles(N);
     // ---- K1: linearisation point ---------------------------------------------------------
-    if (gl < N) {
+    if (cached) {
+        if (gl < N) {
+            S.ub[2 * gl] = stc_in[2 * gl];
+            S.ub[2 * gl + 1] = stc_in[2 * gl + 1];
+        }
+        for (int i = gl; i < 5 * NP; i += GL) S.Xr[i] = stc_in[2 * N + i];
+    } else if (gl < N) {
         if (ubarg) {
             S.ub[2 * gl] = ubarg[(size_t)b * 2 * N + 2 * gl];
             S.ub[2 * gl + 1] = ubarg[(size_t)b * 2 * N + 2 * gl + 1];
@@ -1131,13 +1152,16 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     const double Mtot = (double)(2 * nsoft * N + NBOX * N);
     const double R0 = 2.0 * Pr.w_u1, R1 = 2.0 * Pr.w_u2;
 
-    const int nsqp = Pr.sqp_iters < 0 ? 0 : Pr.sqp_iters;   // 0: return ubar and predict(x0, ubar)
+    // 0: return ubar and predict(x0, ubar).  The split launch (MODE_XO + MODE_IPM) runs single-QP solves
+    // only (launch_solve), so there the SQP loop is a compile-time single pass: nothing is carried across it
+    const int nsqp = MODE != MODE_FULL ? 1 : (Pr.sqp_iters < 0 ? 0 : Pr.sqp_iters);
+    static_assert(MODE == MODE_FULL || MODE == MODE_XO || MODE == MODE_IPM || MODE == MODE_ONE, "launch mode");
     int status = MPC_OK, total_it = 0;
     bool xo_ok = false;                    // MODE_XO: the crossover certified this instance
     double cstr[6] = {0, 0, 0, 0, 0, 0};   // LITE: cost data of stage k (this lane's only)
     for (int sqp = 0; sqp < nsqp; ++sqp) {
-        // ---- K1: nominal rollout == predict(x0, ubar), into Xr ------------------------------
-        predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
+        // ---- K1: nominal rollout == predict(x0, ubar), into Xr (cached: loaded above) ----------
+        if (!cached) predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
         // ---- K2: stage data of QP(ubar) ----------------------------------------------------
         const bool gn = Pr.linearization != 0;
         double refk[5], slk[4];
@@ -1780,18 +1804,44 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
 
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------
     PROF(9)
-    // x0 is re-read here (an opaque index defeats CSE with the first load) rather than held in
-    // registers across the interior point, where it would be spilled to scratch
+    // The instance index and x0 are recomputed / re-read here (from the lane id, the work list and an
+    // opaque index that defeats CSE with the first load) rather than held in registers across the
+    // interior point, where they would be spilled to scratch.
+    int ln2 = __lane_id();
+    asm volatile("" : "+v"(ln2));
+    const int grp2 = ln2 / GL;
     {
-        int bo = b;
-        asm volatile("" : "+v"(bo));
+        if (MODE == MODE_IPM) {
+            const int cnt = *wcount;
+            const int slot = blockIdx.x * G + grp2;
+            bvalid = slot < cnt;
+            b = wlist[bvalid ? slot : cnt - 1];
+        } else {
+            b = blockIdx.x * G + grp2;
+            bvalid = b < B;
+            if (!bvalid) b = B - 1;
+        }
 #pragma unroll
-        for (int j = 0; j < 5; ++j) x0[j] = x0g[5 * (size_t)bo + j];
+        for (int j = 0; j < 5; ++j) x0[j] = x0g[5 * (size_t)b + j];
     }
     predict_grp(tab, N, dt, x0, S.ub, S.Xr, S.kap, gl);
     if (MODE == MODE_XO && !xo_ok) {
-        // not certified: defer to the MODE_IPM launch (group-uniform)
-        if (bvalid && gl == 0) wlist[atomicAdd(wcount, 1)] = b;
+        // not certified: defer to the MODE_IPM launch (group-uniform); S.ub is still the warm start and
+        // S.Xr its rollout (a failed crossover leaves no state behind), which the stage cache keeps
+        int slot = 0;
+        if (bvalid && gl == 0) {
+            slot = atomicAdd(wcount, 1);
+            wlist[slot] = b;
+        }
+        slot = __shfl(slot, grp2 * GL, WAVE);
+        if (bvalid && stc) {
+            double* o = stc + (size_t)slot * stage_cache_doubles(N);
+            if (gl < N) {
+                o[2 * gl] = S.ub[2 * gl];
+                o[2 * gl + 1] = S.ub[2 * gl + 1];
+            }
+            for (int i = gl; i < 5 * NP; i += GL) o[2 * N + i] = S.Xr[i];
+        }
     } else if (bvalid) {
         if (gl < N && Ug) {
             Ug[(size_t)b * 2 * N + 2 * gl] = S.ub[2 * gl];
@@ -1981,6 +2031,12 @@ struct mpc_ctx {
     hipEvent_t wl_done;
     hipStream_t wl_stream;
     bool wl_pending;
+    // stage cache of the split launch (same ordering as the work list): per deferred instance, the
+    // linearisation point and nominal rollout that MODE_XO computed, read back by MODE_IPM.  Grown on
+    // demand by eager calls; a captured call that finds it too small runs without it (same results)
+    double* stc;
+    size_t cap_stc;     // doubles
+    bool use_stc;       // MPC_STAGE_CACHE=0 in the environment disables it (A/B)
 };
 
 extern "C" void mpc_default_params(mpc_params* p) {
@@ -2084,6 +2140,8 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     {
         const char* e = std::getenv("MPC_TWO_PHASE");
         c->two_phase = !(e && e[0] == '0');
+        const char* e2 = std::getenv("MPC_STAGE_CACHE");
+        c->use_stc = !(e2 && e2[0] == '0');
     }
     if (hipMalloc(&c->table_buf, h.size() * sizeof(double)) != hipSuccess) {
         std::free(c);
@@ -2162,6 +2220,7 @@ extern "C" void mpc_destroy(mpc_ctx* c) {
     hipFree(c->ls); hipFree(c->lst); hipFree(c->lct);
     if (c->wl) hipEventDestroy(c->wl_done);
     hipFree(c->wl);
+    hipFree(c->stc);
     hipFree(c->table_buf);
     hipStreamDestroy(c->stream);
     std::free(c);
@@ -2196,10 +2255,21 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (split) HIPCHK(hipStreamIsCapturing(st, &cap), MPC_E_DEVICE);
     const bool capturing = cap != hipStreamCaptureStatusNone;
+    double* stc = nullptr;
     if (split) {
         // the previous split launch may still be reading the list on another stream: order after it
         if (!capturing && c->wl_pending && c->wl_stream != st)
             HIPCHK(hipStreamWaitEvent(st, c->wl_done, 0), MPC_E_DEVICE);
+        const size_t need = (size_t)B * stage_cache_doubles(kp.N);
+        if (c->use_stc && need > c->cap_stc && !capturing) {
+            // hipFree waits for the device, so no launch still reads the old buffer
+            hipFree(c->stc);
+            c->stc = nullptr;
+            c->cap_stc = 0;
+            if (hipMalloc(&c->stc, need * sizeof(double)) == hipSuccess) c->cap_stc = need;
+            else { c->stc = nullptr; (void)hipGetLastError(); }
+        }
+        if (c->use_stc && need <= c->cap_stc) stc = c->stc;
         // reset by a memset on the stream (not by the kernels): a captured graph replays correctly
         HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
     }
@@ -2207,7 +2277,7 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
 #define MPC_LAUNCH(GLV, OBSV, MODEV, NTV)                                                                   \
     hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV, MODEV, NTV>), grid, dim3(WAVE),                    \
                        MODEV == MODE_XO ? lds_lite : lds_wave, st, c->tab, kp, B,                           \
-                       x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt)
+                       x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt, stc)
     // horizon-specialised kernels for the BASELINE horizons that pay for their code size (N = 20)
 #define MPC_LAUNCH_GL(MODEV)                                                                   \
     do {                                                                                       \
@@ -2227,6 +2297,8 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
             c->wl_stream = st;
             c->wl_pending = true;
         }
+    } else if (kp.sqp_iters == 1) {
+        MPC_LAUNCH_GL(MODE_ONE);
     } else {
         MPC_LAUNCH_GL(MODE_FULL);
     }
