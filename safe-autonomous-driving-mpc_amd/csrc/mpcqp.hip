@@ -28,6 +28,9 @@
 #include "host_table.h"
 
 #define WAVE 64
+#ifndef MPC_NTR32
+#define MPC_NTR32 0       // experiment: unrolled solves in the GL = 32 obstacle kernels too
+#endif
 #ifndef MPC_NO_NT20
 #define MPC_NO_NT20 0
 #endif
@@ -1051,10 +1054,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                  double* __restrict__ stc) {
     constexpr int G = WAVE / GL;
     constexpr int NR = OBS ? NROW : NROW - 2;    // soft rows held per lane (6, 7: obstacle rows)
-    // the Riccati solves are fully unrolled (compile-time horizon) in the obstacle-free kernels only:
-    // the obstacle kernels hold 9 rows per lane, and there the looped solves need fewer registers
-    // (fewer spills; measured C3 1.34 -> 1.24 ms)
-    constexpr int NTR = OBS ? 0 : NT;
+    // the Riccati solves are fully unrolled (compile-time horizon) except in the GL = 32 obstacle kernels:
+    // there the lanes hold 9 rows each, and the looped solves need fewer registers (fewer spills;
+    // measured C3 1.34 -> 1.24 ms in round 1).  The GL = 64 obstacle kernel (N = 40, C5) unrolls them:
+    // C5 5.67 -> 4.16 ms together with the unrolled factorisation of NT = 40
+    constexpr int NTR = (OBS && GL == 32 && !MPC_NTR32) ? 0 : NT;
     // row right-hand sides recomputed after the solve (WRC) instead of held live across it: obstacle
     // kernels only (measured neutral on the obstacle-free N = 20 kernel)
     constexpr bool WRC = OBS;
@@ -2235,7 +2239,10 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     const int GL = kp.N + 1 <= 16 ? 16 : (kp.N + 1 <= 32 ? 32 : 64);
     const int G = WAVE / GL;
     const bool nt20 = kp.N == 20 && !MPC_NO_NT20;
-    const size_t lds_wave = sizeof(double) * (size_t)lds_doubles(kp.N, acl_on(GL, nt20 ? 20 : 0)) * G;
+    const bool nt40 = kp.N == 40 && !MPC_NO_NT20;
+    const bool nt30 = kp.N == 30 && !MPC_NO_NT20;
+    const int ntv = nt20 ? 20 : (nt40 ? 40 : (nt30 ? 30 : 0));
+    const size_t lds_wave = sizeof(double) * (size_t)lds_doubles(kp.N, acl_on(GL, ntv)) * G;
     if (lds_wave > 160 * 1024) return fail(MPC_E_ARG, "horizon too long for LDS");
     const size_t lds_lite = sizeof(double) * (size_t)lds_doubles(kp.N, false, true) * G;   // MODE_XO
     const dim3 grid((B + G - 1) / G);
@@ -2278,10 +2285,13 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV, MODEV, NTV>), grid, dim3(WAVE),                    \
                        MODEV == MODE_XO ? lds_lite : lds_wave, st, c->tab, kp, B,                           \
                        x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt, stc)
-    // horizon-specialised kernels for the BASELINE horizons that pay for their code size (N = 20)
+    // horizon-specialised kernels for the BASELINE horizons (N = 20: C2, C3; N = 30: C4; N = 40: C5), whose
+    // unrolled recursions pay for their code size (C4 0.89 -> 0.66 ms, C5 5.67 -> 4.16 ms)
 #define MPC_LAUNCH_GL(MODEV)                                                                   \
     do {                                                                                       \
         if (nt20) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 20); else MPC_LAUNCH(32, false, MODEV, 20); } \
+        else if (nt30) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 30); else MPC_LAUNCH(32, false, MODEV, 30); } \
+        else if (nt40) { if (with_obs) MPC_LAUNCH(64, true, MODEV, 40); else MPC_LAUNCH(64, false, MODEV, 40); } \
         else if (GL == 16) { if (with_obs) MPC_LAUNCH(16, true, MODEV, 0); else MPC_LAUNCH(16, false, MODEV, 0); } \
         else if (GL == 32) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 0); else MPC_LAUNCH(32, false, MODEV, 0); } \
         else { if (with_obs) MPC_LAUNCH(64, true, MODEV, 0); else MPC_LAUNCH(64, false, MODEV, 0); } \
