@@ -28,9 +28,6 @@
 #include "host_table.h"
 
 #define WAVE 64
-#ifndef MPC_NTR32
-#define MPC_NTR32 0       // experiment: unrolled solves in the GL = 32 obstacle kernels too
-#endif
 #ifndef MPC_NO_NT20
 #define MPC_NO_NT20 0
 #endif
@@ -1054,11 +1051,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                  double* __restrict__ stc) {
     constexpr int G = WAVE / GL;
     constexpr int NR = OBS ? NROW : NROW - 2;    // soft rows held per lane (6, 7: obstacle rows)
-    // the Riccati solves are fully unrolled (compile-time horizon) except in the GL = 32 obstacle kernels:
-    // there the lanes hold 9 rows each, and the looped solves need fewer registers (fewer spills;
-    // measured C3 1.34 -> 1.24 ms in round 1).  The GL = 64 obstacle kernel (N = 40, C5) unrolls them:
-    // C5 5.67 -> 4.16 ms together with the unrolled factorisation of NT = 40
-    constexpr int NTR = (OBS && GL == 32 && !MPC_NTR32) ? 0 : NT;
+    // the Riccati solves of the horizon-specialised kernels are fully unrolled, obstacle kernels included.
+    // (Round 1 kept them looped in the obstacle kernels, whose lanes hold 9 rows, for fewer spills; since
+    // the split kernels carry no runtime SQP loop, unrolled is faster there too: C4 0.660 -> 0.609 ms,
+    // C3 -0.8%, and C5 5.67 -> 4.16 ms together with the unrolled factorisation of NT = 40.)
+    constexpr int NTR = NT;
     // row right-hand sides recomputed after the solve (WRC) instead of held live across it: obstacle
     // kernels only (measured neutral on the obstacle-free N = 20 kernel)
     constexpr bool WRC = OBS;
