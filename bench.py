@@ -52,6 +52,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=4, metavar="K",
                     help="secondary serving leg: K independent batches of the same shape in flight on K streams "
                          "(one solver context each); reported as 'inflight', never as 'value' (0: skip)")
+    ap.add_argument("--nlp-steps", type=int, default=5, metavar="K",
+                    help="secondary leg: K batches of the same egos solved with the drop-in default (Gauss-Newton "
+                         "SQP to the reference NLP optimum, trajectory_tracking.SQP_ITERS / sqp_tol); 0: skip")
     ap.add_argument("--closed-loop", type=int, default=0, metavar="B",
                     help="also run B egos through the device closed loop (mpc_closed_loop, SURVEY 8(f)1) on the "
                          "config's trajectory and FSM preset and report closed-loop ego-steps/s")
@@ -195,6 +198,8 @@ def main():
                                  "PMC HBM bytes per step (profiles/pmc_hbm_bytes.json)",
                          "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
         }
+        if args.nlp_steps > 0:
+            out["nlp_sqp"] = nlp_leg(args.nlp_steps, wb, B, N, mo, X, U, dev)
         if args.inflight > 1:
             head = {k: v.cpu().numpy() for k, v in (("st", st), ("it", it), ("U", Uo))}
             out["inflight"] = inflight(args.inflight, args.steps, wb, B, N, mo, X, U, dev, head)
@@ -206,6 +211,45 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def nlp_leg(steps, wb, B, N, mo, X, U, dev):
+    """Secondary leg (not `value`): the same egos through the drop-in default of the Python surface,
+    i.e. the Gauss-Newton SQP that converges to the optimum of the reference's nonlinear problem
+    (tests/test_gpu_nlp.py pins it to nlp_golden); one batch at a time, HIP events on the launch stream."""
+    import numpy as np
+    import torch
+    import mpcqp
+    import trajectory_tracking as TT
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    ptr = lambda x: 0 if x is None else x.data_ptr()
+    p = mpcqp.default_params(N=N, max_obs=mo, sqp_iters=TT.SQP_ITERS)
+    slv = mpcqp.Solver(X, U, p, device=dev.index)
+    x0 = t(wb["x0"])
+    obs = t(wb["obs"]) if wb["obs"] is not None else None
+    nob = t(wb["n_obs"], torch.int32) if wb["n_obs"] is not None else None
+    o = [torch.empty((B, 2), dtype=torch.float64, device=dev), torch.empty((B, N, 2), dtype=torch.float64, device=dev),
+         torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev), torch.empty(B, dtype=torch.int32, device=dev),
+         torch.empty(B, dtype=torch.int32, device=dev)]
+    stream = torch.cuda.current_stream(dev)
+    call = lambda: slv.solve_batch_device(B, ptr(x0), ptr(obs), ptr(nob), 0, *[ptr(a) for a in o],
+                                          stream=stream.cuda_stream)
+    call()
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    ev[0].record(stream)
+    for i in range(steps):
+        call()
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])
+    st, it = o[3].cpu().numpy(), o[4].cpu().numpy()
+    slv.close()
+    return {"value": B * steps / (ms.sum() / 1e3), "unit": "solves/s", "ms_per_batch": float(ms.mean()),
+            "p50_batch_latency_ms": float(np.median(ms)), "sqp_iters_cap": TT.SQP_ITERS, "sqp_tol": p.sqp_tol,
+            "mean_pdip_iters": float(it.mean()), "status_counts": np.bincount(st, minlength=4).tolist(),
+            "note": "drop-in default of the Python surface (TrajectoryTracker.solve): SQP re-linearisations until "
+                    "U moves by <= sqp_tol; secondary, the headline is the single tracking QP"}
 
 
 def inflight(K, steps, wb, B, N, mo, X, U, dev, head):
