@@ -362,6 +362,31 @@ def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_ego
                     "answer)"}
 
 
+def cpu_baseline(wb, N, mo, budget_s):
+    """The oracle's C restatement (same QP, same PDIP), OpenMP over the host CPUs this process may use, on
+    a bounded sample of the same egos.  kind = 'port' (the reference itself never travels to the GPU box)."""
+    import oracle as O
+    import workloads as W
+    ld = W.loader(wb["traj"])
+    orc = O.Oracle(ld.X_ref, ld.U_ref)
+    p = O.default_params(N=N, max_obs=mo)
+    hw = host_cores()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hw["affinity_cpus"]
+    n = min(512, wb["x0"].shape[0])
+    sl = slice(0, n)
+    obs = None if wb["obs"] is None else wb["obs"][sl]
+    nob = None if wb["n_obs"] is None else wb["n_obs"][sl]
+    orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)        # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)
+        done += n
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port", "host": hw,
+            "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by the oracle's C PDIP "
+                      f"(oracle/mpc_oracle.c) with OpenMP, {threads} threads"}
+
+
 def host_cores():
     """Host CPUs as the GPU box shows them: physical cores (lscpu, unique core/socket pairs) of the whole
     machine, and the CPUs this process may run on (its affinity mask: the box's share)."""
