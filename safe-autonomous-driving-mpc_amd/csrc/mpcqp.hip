@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1844,14 +1845,13 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int i = gl; i < 5 * NP; i += GL) o[2 * N + i] = S.Xr[i];
         }
     } else if (bvalid) {
-        if (gl < N && Ug) {
-            Ug[(size_t)b * 2 * N + 2 * gl] = S.ub[2 * gl];
-            Ug[(size_t)b * 2 * N + 2 * gl + 1] = S.ub[2 * gl + 1];
-        }
+        // one 16-B store per lane (full cache lines, not two half-filled strided stores)
+        if (gl < N && Ug)
+            *reinterpret_cast<double2*>(Ug + (size_t)b * 2 * N + 2 * gl) = make_double2(S.ub[2 * gl], S.ub[2 * gl + 1]);
         if (Xg)
             for (int i = gl; i < 5 * NP; i += GL) Xg[(size_t)b * 5 * NP + i] = S.Xr[i];
         if (gl == 0) {
-            if (u0g) { u0g[2 * (size_t)b] = S.ub[0]; u0g[2 * (size_t)b + 1] = S.ub[1]; }
+            if (u0g) *reinterpret_cast<double2*>(u0g + 2 * (size_t)b) = make_double2(S.ub[0], S.ub[1]);
             if (statusg) statusg[b] = status;
             if (itersg) itersg[b] = total_it;
         }
@@ -2033,11 +2033,14 @@ struct mpc_ctx {
     hipStream_t wl_stream;
     bool wl_pending;
     // stage cache of the split launch (same ordering as the work list): per deferred instance, the
-    // linearisation point and nominal rollout that MODE_XO computed, read back by MODE_IPM.  Grown on
-    // demand by eager calls; a captured call that finds it too small runs without it (same results)
+    // linearisation point and nominal rollout that MODE_XO computed, read back by MODE_IPM.  Off by
+    // default (MPC_STAGE_CACHE=1 enables it): the repeated setup is ~1% of the slowest instance, and the
+    // A/B is within noise (C2 0.4288 vs 0.4288 ms, C3 0.4977 vs 0.5004, C4 0.6078 vs 0.6107, two runs
+    // each) while the cache moves 2.9 MB more per C2 step.  Grown on demand by eager calls; a captured
+    // call that finds it too small runs without it (same results)
     double* stc;
     size_t cap_stc;     // doubles
-    bool use_stc;       // MPC_STAGE_CACHE=0 in the environment disables it (A/B)
+    bool use_stc;
 };
 
 extern "C" void mpc_default_params(mpc_params* p) {
@@ -2142,7 +2145,7 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         const char* e = std::getenv("MPC_TWO_PHASE");
         c->two_phase = !(e && e[0] == '0');
         const char* e2 = std::getenv("MPC_STAGE_CACHE");
-        c->use_stc = !(e2 && e2[0] == '0');
+        c->use_stc = e2 && e2[0] == '1';
     }
     if (hipMalloc(&c->table_buf, h.size() * sizeof(double)) != hipSuccess) {
         std::free(c);
@@ -2325,6 +2328,8 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
     if (c->p.max_obs > 0 && n_obs && !obs) return fail(MPC_E_ARG, "n_obs given but obs is NULL");
     if (obs && c->p.max_obs == 0)
         return fail(MPC_E_ARG, "obs given but params.max_obs == 0 (the obstacles would be ignored)");
+    if (((uintptr_t)u0 | (uintptr_t)U) & 15)
+        return fail(MPC_E_ARG, "u0 and U must be 16-byte aligned (hipMalloc and torch allocations are)");
     int rc = check_params(&c->p);
     if (rc) return rc;
     KParams kp = kparams(&c->p);
