@@ -1882,14 +1882,60 @@ struct ClState {
     double* x;          // [B][5]    current state
     double* obs;        // [B][2][2] obstacle slab of this step (car first, then the light: :341-358)
     int* nobs;          // [B]
-    double* u0;         // [B][2]
-    int* status;        // [B]
     int* active;        // [B]       still inside the loop condition s <= s_stop (:395)
     double* obs_s;      // [B]       dynamic obstacle position
     double* tl_timer;   // [B]
     int* fsm_flags;     // [B][4]    obs_active, obs_has_triggered, tl_green, tl_waiting
     int* n_active;      // [1]
+    // the solver runs on the egos still in the loop only: alist [B] holds their ids (increasing, rebuilt by
+    // cl_compact_kernel whenever egos have left), and the solve reads / writes the packed slabs below
+    int* alist;         // [B]
+    int* n_list;        // [1]
+    double* xa;         // [B][5]
+    double* obsa;       // [B][2][2]
+    int* nobsa;         // [B]
+    double* u0a;        // [B][2]
+    int* sta;           // [B]
 };
+
+// ids of the egos still in the loop, in increasing order (deterministic): one workgroup of 1024 lanes,
+// wave ballots and a scan of the 16 wave counts per chunk
+__global__ void __launch_bounds__(1024) cl_compact_kernel(int B, ClState C) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int c0 = 0; c0 < B; c0 += 1024) {
+        const int e = c0 + threadIdx.x;
+        const bool f = e < B && C.active[e];
+        const unsigned long long m = __ballot(f);
+        const int pre = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int i = 0; i < w; ++i) off += wsum[i];
+        if (f) C.alist[off + pre] = e;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int t = 0;
+            for (int i = 0; i < 16; ++i) t += wsum[i];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *C.n_list = base;
+}
+
+// packs the listed egos' state and obstacle slab for the solve (slot i <- ego alist[i])
+__global__ void cl_gather_kernel(int nl, ClState C) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const int e = C.alist[i];
+    for (int j = 0; j < 5; ++j) C.xa[5 * (size_t)i + j] = C.x[5 * (size_t)e + j];
+    for (int j = 0; j < 4; ++j) C.obsa[4 * (size_t)i + j] = C.obs[4 * (size_t)e + j];
+    C.nobsa[i] = C.nobs[e];
+}
 
 // ObstaclesFSM.update(dt, s, v) (trajectory_tracking.py:330-374) for every active ego
 __global__ void cl_fsm_kernel(int B, mpc_fsm F, double dt, ClState C, double* hist_obs_s, int* hist_tl, int step,
@@ -1935,15 +1981,18 @@ __global__ void cl_fsm_kernel(int B, mpc_fsm F, double dt, ClState C, double* hi
     if (hist_tl) hist_tl[(size_t)b * max_steps + step] = fl[2];
 }
 
-// plant step x <- x + dt * dynamics(x, u0, k_ref(x_s)) (:403-406) and the histories (:412-421)
-__global__ void cl_plant_kernel(DevTable tab, int B, double dt, ClState C, double s_stop, double* hist_x,
+// plant step x <- x + dt * dynamics(x, u0, k_ref(x_s)) (:403-406) and the histories (:412-421), for the
+// listed egos (slot i: ego alist[i], its control at u0a[i])
+__global__ void cl_plant_kernel(DevTable tab, int nl, double dt, ClState C, double s_stop, double* hist_x,
                                 double* hist_u, int* hist_status, int* n_steps, int step, int max_steps) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B || !C.active[b]) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const int b = C.alist[i];
+    if (!C.active[b]) return;
     double x[5], st[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) x[j] = C.x[5 * (size_t)b + j];
-    const double u1 = C.u0[2 * (size_t)b], u2 = C.u0[2 * (size_t)b + 1];
+    const double u1 = C.u0a[2 * (size_t)i], u2 = C.u0a[2 * (size_t)i + 1];
     get_state(tab, x[0], st, nullptr);
     const double xd[5] = {x[4], x[4] * x[2], x[4] * (x[3] - st[3]), u1, u2};
 #pragma unroll
@@ -1956,7 +2005,7 @@ __global__ void cl_plant_kernel(DevTable tab, int B, double dt, ClState C, doubl
         hist_u[((size_t)b * max_steps + step) * 2] = u1;
         hist_u[((size_t)b * max_steps + step) * 2 + 1] = u2;
     }
-    if (hist_status) hist_status[(size_t)b * max_steps + step] = C.status[b];
+    if (hist_status) hist_status[(size_t)b * max_steps + step] = C.sta[i];
     n_steps[b] = step + 1;
     if (!(x[0] <= s_stop)) C.active[b] = 0;
     else atomicAdd(C.n_active, 1);
@@ -2431,13 +2480,18 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
     C.x = (double*)dalloc(nb * 5 * 8);
     C.obs = (double*)dalloc(nb * 4 * 8);
     C.nobs = (int*)dalloc(nb * 4);
-    C.u0 = (double*)dalloc(nb * 2 * 8);
-    C.status = (int*)dalloc(nb * 4);
     C.active = (int*)dalloc(nb * 4);
     C.obs_s = (double*)dalloc(nb * 8);
     C.tl_timer = (double*)dalloc(nb * 8);
     C.fsm_flags = (int*)dalloc(nb * 4 * 4);
     C.n_active = (int*)dalloc(4);
+    C.alist = (int*)dalloc(nb * 4);
+    C.n_list = (int*)dalloc(4);
+    C.xa = (double*)dalloc(nb * 5 * 8);
+    C.obsa = (double*)dalloc(nb * 4 * 8);
+    C.nobsa = (int*)dalloc(nb * 4);
+    C.u0a = (double*)dalloc(nb * 2 * 8);
+    C.sta = (int*)dalloc(nb * 4);
     double* d_xinit = (double*)dalloc(nb * 5 * 8);
     double* d_hx = hist_x ? (double*)dalloc(nb * (ns + 1) * 5 * 8) : nullptr;
     double* d_hu = hist_u ? (double*)dalloc(nb * ns * 2 * 8) : nullptr;
@@ -2488,17 +2542,27 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
     }
     int steps_run = 0;
     rc = MPC_SUCCESS;
-    for (int step = 0; step < max_steps; ++step) {
+    // the solve runs on the egos still in the loop: the list is rebuilt at the host syncs below whenever
+    // egos have left, so retired egos stop costing solver work (results are per ego, unchanged)
+    hipLaunchKernelGGL(cl_compact_kernel, dim3(1), dim3(1024), 0, st, B, C);
+    int nl = 0;
+    if (hipMemcpyAsync(&nl, C.n_list, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        cleanup();
+        return fail(MPC_E_DEVICE, "closed-loop initial ego list");
+    }
+    for (int step = 0; step < max_steps && nl > 0; ++step) {
         // runs without scenarios too: records the RED light / no-car histories like the reference
         hipLaunchKernelGGL(cl_fsm_kernel, tg, tb, 0, st, B, F, kp.dt, C, d_ho, d_ht, step, max_steps);
-        rc = launch_solve(c, kp, B, C.x, with_fsm ? C.obs : nullptr, with_fsm ? C.nobs : nullptr, nullptr, C.u0,
-                          nullptr, nullptr, C.status, nullptr, st);
+        const dim3 lg((nl + 255) / 256);
+        hipLaunchKernelGGL(cl_gather_kernel, lg, tb, 0, st, nl, C);
+        rc = launch_solve(c, kp, nl, C.xa, with_fsm ? C.obsa : nullptr, with_fsm ? C.nobsa : nullptr, nullptr, C.u0a,
+                          nullptr, nullptr, C.sta, nullptr, st);
         if (rc) break;
         if (hipMemsetAsync(C.n_active, 0, 4, st) != hipSuccess) {
             rc = fail(MPC_E_DEVICE, "closed-loop active-count reset");
             break;
         }
-        hipLaunchKernelGGL(cl_plant_kernel, tg, tb, 0, st, c->tab, B, kp.dt, C, s_stop, d_hx, d_hu, d_hs, d_ns, step,
+        hipLaunchKernelGGL(cl_plant_kernel, lg, tb, 0, st, c->tab, nl, kp.dt, C, s_stop, d_hx, d_hu, d_hs, d_ns, step,
                            max_steps);
         if (step_ms && hipEventRecord(ev[step + 1], st) != hipSuccess) {
             rc = fail(MPC_E_DEVICE, "hipEventRecord (step timing)");
@@ -2513,6 +2577,14 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
                 break;
             }
             if (na == 0) break;
+            if (na < nl) {                                  // egos left: shrink the solver's list
+                hipLaunchKernelGGL(cl_compact_kernel, dim3(1), dim3(1024), 0, st, B, C);
+                if (hipMemcpyAsync(&nl, C.n_list, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess) {
+                    rc = fail(MPC_E_DEVICE, "closed-loop ego list");
+                    break;
+                }
+            }
         }
     }
     if (rc == MPC_SUCCESS && hipGetLastError() != hipSuccess) rc = fail(MPC_E_LAUNCH, "closed-loop kernel launch");

@@ -99,3 +99,25 @@ def test_batch_equals_single_runs(tt):
         assert n == int(r["n_steps"][b])
         assert np.array_equal(r1["hist_x"][0, :n + 1], r["hist_x"][b, :n + 1])
     assert np.isfinite(r["step_ms"][:int(r["n_steps"].max())]).all()
+
+
+def test_egos_leaving_at_different_steps(tt):
+    """Egos that leave the loop early stop costing solver work (the solver's ego list is compacted at the
+    host syncs): a batch whose egos finish at very different steps still equals each ego run alone, and the
+    host loop, bit for bit."""
+    TT, TL, bt = tt
+    traj = TL(bt(1))
+    mpc = TT.TrajectoryTracker(traj)
+    mpc.N = 10
+    starts = [0.0, 120.0, 250.0, 297.0, 60.0, 280.0, 10.0]
+    x_init = np.array([[s, 0.02, 0.0, traj.get_state(s)[3], 3.0] for s in starts])
+    r = TT.run_simulation_batch(mpc, TT.ObstaclesFSM(), traj, x_init=x_init, max_steps=400)
+    ns = r["n_steps"]
+    assert len(set(ns.tolist())) >= 5 and ns.min() < 20 and ns.max() > 100
+    for b in range(len(starts)):
+        r1 = TT.run_simulation_batch(mpc, TT.ObstaclesFSM(), traj, x_init=x_init[b:b + 1], max_steps=400)
+        n = int(r1["n_steps"][0])
+        assert n == int(ns[b])
+        assert np.array_equal(r1["hist_x"][0, :n + 1], r["hist_x"][b, :n + 1])
+        assert np.array_equal(r1["hist_u"][0, :n], r["hist_u"][b, :n])
+    compare(r, 3, host_loop(TT, mpc, TT.ObstaclesFSM(), traj, x_init[3], 400))
