@@ -26,7 +26,7 @@ import numpy as np
 import mpcqp
 from sanity_checks import trajectory_tracking_check
 
-# Gauss-Newton SQP cap of the drop-in default: sqp_tol stops it earlier, after 5-8 QPs on 55 of the 57
+# Gauss-Newton SQP cap of the drop-in default: sqp_tol stops it earlier, after 5-8 QPs on 50 of the 52
 # certified nlp_golden cases; the slowest (a braking start far inside the obstacle margin) needs 28
 SQP_ITERS = 30
 

@@ -1,0 +1,61 @@
+"""Static resources of the built solver kernels (CPU test: reads the gfx950 code object's metadata from
+libmpcqp.so with the ROCm LLVM tools, tools/kernel_resources.py).
+
+The library is built with -Wno-pass-failed (the runtime-horizon kernels request unrolls over opaque trip
+counts), so a full unroll that silently fails in a horizon-specialised kernel would not warn; it would
+turn the unrolled ping-pong records into dynamically indexed arrays and show up as scratch.  Pinned here:
+  - the C2 path (crossover kernel + interior-point kernel, N = 20, no obstacles) uses no scratch at all;
+  - no crossover kernel uses scratch;
+  - the horizon-specialised single-QP kernels (split pair and one-launch, NT = 20, 30, 40) stay at the
+    small spills measured in round 3 (<= 128 B per lane; they were 148-412 B before the split kernels lost
+    their runtime SQP loop);
+  - no kernel exceeds 512 B per lane.
+"""
+import os
+
+import pytest
+
+from conftest import ROOT
+
+LIB = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcqp.so")
+
+
+@pytest.fixture(scope="module")
+def kernels():
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf"):
+        pytest.skip("ROCm LLVM tools not available")
+    import __graft_entry__ as g
+    g.build()
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_resources import kernel_resources, solver_kernel_key
+    out = {}
+    for k in kernel_resources(LIB):
+        key = solver_kernel_key(k["name"])
+        if key:
+            out[key] = k
+    return out
+
+
+def test_all_solver_instantiations_present(kernels):
+    # GL x OBS x MODE x NT: runtime horizon for GL 16/32/64, NT = 20, 30 (GL 32) and 40 (GL 64)
+    assert len(kernels) == 48
+
+
+def test_c2_path_has_no_scratch(kernels):
+    assert kernels[(32, 0, 1, 20)]["scratch"] == 0          # crossover kernel
+    assert kernels[(32, 0, 2, 20)]["scratch"] == 0          # interior-point kernel
+
+
+def test_crossover_kernels_have_no_scratch(kernels):
+    for key, k in kernels.items():
+        if key[2] == 1:
+            assert k["scratch"] == 0, (key, k)
+
+
+def test_specialised_single_qp_kernels_spill_little(kernels):
+    for key, k in kernels.items():
+        gl, obs, mode, nt = key
+        if nt > 0 and mode in (1, 2, 3):
+            assert k["scratch"] <= 128, (key, k)
+        assert k["scratch"] <= 512, (key, k)
