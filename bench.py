@@ -249,7 +249,7 @@ def nlp_leg(steps, wb, B, N, mo, X, U, dev):
             "p50_batch_latency_ms": float(np.median(ms)), "sqp_iters_cap": TT.SQP_ITERS, "sqp_tol": p.sqp_tol,
             "mean_pdip_iters": float(it.mean()), "status_counts": np.bincount(st, minlength=4).tolist(),
             "note": "drop-in default of the Python surface (TrajectoryTracker.solve): SQP re-linearisations until "
-                    "U moves by <= sqp_tol; secondary, the headline is the single tracking QP"}
+                    "U moves by <= sqp_tol (or a 2-cycle / 5 elastic QPs in a row, include/mpcqp.h); secondary, the headline is the single tracking QP"}
 
 
 def inflight(K, steps, wb, B, N, mo, X, U, dev, head):

@@ -72,7 +72,10 @@ typedef struct mpc_params {
     double tol_mu;                  /* absolute complementarity tolerance                             */
     double elastic_rho;             /* L1 penalty of the elastic (soft) state rows                    */
     double sqp_tol;                 /* SQP stops early once a re-linearised QP moves U by at most this
-                                       (max-norm); 0 = always run sqp_iters QPs                        */
+                                       (max-norm), and also (sqp_tol > 0) on a 2-cycle, i.e. a QP that
+                                       returns U of two QPs back (|U_k - U_k-2| <= 1e-6 |U_k - U_k-1|),
+                                       and after 5 elastic (infeasible) QPs in a row; 0 = always run
+                                       sqp_iters QPs                                                  */
 } mpc_params;
 
 typedef struct mpc_ctx mpc_ctx;

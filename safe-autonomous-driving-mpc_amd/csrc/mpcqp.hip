@@ -1012,6 +1012,10 @@ __device__ unsigned long long g_prof[16];
 #define POLISH_REFINE 2
 #define POLISH_ROUNDS 6
 #define XO_ROUNDS 1            // rounds of the crossover attempt before the interior point
+// SQP stopping rules besides convergence (oracle orc_solve): a 2-cycle (the QP returns the point of two QPs
+// back, |U_k - U_k-2| <= SQP_CYCLE_REL |U_k - U_k-1|), and SQP_INF_STREAK elastic QPs in a row
+#define SQP_CYCLE_REL 1e-6
+#define SQP_INF_STREAK 5
 #define MU0 1000.0
 
 // ------------------------------------------------------------------------------------------
@@ -1159,6 +1163,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     const int nsqp = MODE != MODE_FULL ? 1 : (Pr.sqp_iters < 0 ? 0 : Pr.sqp_iters);
     static_assert(MODE == MODE_FULL || MODE == MODE_XO || MODE == MODE_IPM || MODE == MODE_ONE, "launch mode");
     int status = MPC_OK, total_it = 0;
+    // SQP state carried across re-linearisations (MODE_FULL): the row / box classification the last polish
+    // left (2 bits per row, then one per box row), which starts the next QP's crossover (oracle polish_from,
+    // given = 2); U two QPs back at this lane's control; the count of elastic QPs in a row
+    int wcls = 0, ninf = 0;
+    double pb0 = 0.0, pb1 = 0.0;
     bool xo_ok = false;                    // MODE_XO: the crossover certified this instance
     double cstr[6] = {0, 0, 0, 0, 0, 0};   // LITE: cost data of stage k (this lane's only)
     for (int sqp = 0; sqp < nsqp; ++sqp) {
@@ -1628,6 +1637,13 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int j = 0; j < NR; ++j) cls[j] = !ron[j] ? 0 : (rxi[j] > rnu[j] ? 2 : (rl[j] > rs[j] ? 1 : 0));
 #pragma unroll
             for (int j = 0; j < NBOX; ++j) clb[j] = (live && lb[j] > sb[j]) ? 1 : 0;
+            if (MODE == MODE_FULL && phase == 0 && sqp > 0) {
+                // re-linearisation: the crossover starts from the previous QP's classification
+#pragma unroll
+                for (int j = 0; j < NR; ++j) cls[j] = ron[j] ? (wcls >> (2 * j)) & 3 : 0;
+#pragma unroll
+                for (int j = 0; j < NBOX; ++j) clb[j] = live ? (wcls >> (2 * NR + j)) & 1 : 0;
+            }
             // the interior-point iterate (du, x4) is the start of every round and the fallback
             double pu0 = du0, pu1 = du1;
             double nviol_acc = 0.0;
@@ -1784,6 +1800,13 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     if (flipb[j]) clb[j] = 1 - clb[j];
                 wave_sync();
             }
+            if (MODE == MODE_FULL && nsqp > 1) {
+                wcls = 0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j) wcls |= cls[j] << (2 * j);
+#pragma unroll
+                for (int j = 0; j < NBOX; ++j) wcls |= clb[j] << (2 * NR + j);
+            }
             if (accepted) {
                 du0 = pu0;
                 du1 = pu1;
@@ -1795,13 +1818,25 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         if (accepted || phase == 1) break;
         }   // phases
         status = st_here;
+        double ua0 = 0.0, ua1 = 0.0;       // this QP's linearisation point: U one QP back
         if (live) {
-            S.ub[2 * (k - 1)] += du0;
-            S.ub[2 * (k - 1) + 1] += du1;
+            ua0 = S.ub[2 * (k - 1)];
+            ua1 = S.ub[2 * (k - 1) + 1];
+            S.ub[2 * (k - 1)] = ua0 + du0;
+            S.ub[2 * (k - 1) + 1] = ua1 + du1;
         }
         wave_sync();
-        // SQP: stop once the re-linearised QP no longer moves U (oracle orc_solve; group-uniform)
-        if (nsqp > 1 && Q.max(live ? vmaxabs(fabs(du0), du1) : 0.0) <= Pr.sqp_tol) break;
+        // SQP: stop once the re-linearised QP no longer moves U, on a 2-cycle, or after SQP_INF_STREAK elastic
+        // QPs in a row (oracle orc_solve; all group-uniform)
+        if (nsqp > 1) {
+            const double stp = Q.max(live ? vmaxabs(fabs(du0), du1) : 0.0);
+            const double b2 = Q.max(live ? vmaxabs(fabs((ua0 + du0) - pb0), (ua1 + du1) - pb1) : 0.0);
+            pb0 = ua0;
+            pb1 = ua1;
+            ninf = status == MPC_INFEASIBLE ? ninf + 1 : 0;
+            if (stp <= Pr.sqp_tol) break;
+            if (Pr.sqp_tol > 0.0 && ((sqp >= 2 && b2 <= SQP_CYCLE_REL * stp) || ninf >= SQP_INF_STREAK)) break;
+        }
     }
 
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------

@@ -13,7 +13,8 @@ Reference: medinammartin3/Safe-Autonomous-Driving-MPC trajectory_tracking.py
 What differs by design: the reference's SLSQP on the nonlinear problem
 (ftol 1e-3, maxiter 15, finite-difference gradients) is replaced by a Gauss-Newton SQP from the
 same warm start: each QP is solved to 1e-9 by a primal-dual interior point on the GPU and re-linearised
-about its solution until U moves by at most `sqp_tol` (at most `sqp_iters` QPs).  By default solve()
+about its solution until U moves by at most `sqp_tol` (at most `sqp_iters` QPs; it also stops on a 2-cycle
+and after 5 elastic QPs in a row, include/mpcqp.h).  By default solve()
 therefore returns the optimum of the reference's own nonlinear problem (pinned to it by
 tests/golden/nlp_golden.npz), which its SLSQP only approximates; `sqp_iters = 1` gives the single
 tracking QP at the warm start that bench.py times.  There is no CPU fallback: without libmpcqp.so or a

@@ -25,7 +25,11 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:abort_on_err
 
 @pytest.fixture(scope="module")
 def drivers():
-    r = subprocess.run(["make", "-C", ASAN], capture_output=True, text=True)
+    # one build at a time: pytest-xdist workers share the tree, and a worker must not run a driver
+    # while another one relinks it
+    from filelock import FileLock
+    with FileLock(os.path.join(ASAN, ".build.lock")):
+        r = subprocess.run(["make", "-C", ASAN], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     return os.path.join(ASAN, "json_driver"), os.path.join(ASAN, "oracle_driver")
 

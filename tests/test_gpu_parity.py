@@ -151,7 +151,7 @@ def elastic_objective(orc, p, x0, obs, U):
     return 0.5 * du @ q["H"] @ du + q["f"] @ du + q["c0"] + p.elastic_rho * viol.sum()
 
 
-def check_vs_oracle(r, ro, ctx=None, label="", tol=TOL_U):
+def check_vs_oracle(r, ro, ctx=None, label="", tol=TOL_U, xtol=1e-8):
     """Status and U/Xpred parity, returns the summary dict (printed by the callers).
     Statuses must agree, except flips between infeasible (2) and numerical (3): both mean "no certified
     solution of the hard QP"; they happen on badly infeasible elastic problems (rho = 1e5), where the last
@@ -184,7 +184,7 @@ def check_vs_oracle(r, ro, ctx=None, label="", tol=TOL_U):
         alt += 1
     ok = cert & (err <= tol)
     xe = np.abs(r["Xpred"] - ro["Xpred"]).reshape(len(cert), -1).max(axis=1)
-    assert xe[ok].max(initial=0.0) <= 1e-8, (label, xe[ok].max())
+    assert xe[ok].max(initial=0.0) <= xtol, (label, xe[ok].max())
     s = dict(label=label, B=len(cert), status_agree=float(agree.mean()), flips_2_3=int(mism.sum()),
              elastic_alt_optima=alt, max_err_U=float(err[ok].max(initial=0.0)),
              max_err_Xpred=float(xe[ok].max(initial=0.0)))
@@ -224,8 +224,9 @@ def test_sqp_relinearisation_vs_oracle(lib, solvers, cfg, B, nsqp):
     po = O.default_params(N=wb["N"], max_obs=wb["max_obs"], sqp_iters=nsqp)
     ro = orc.solve_batch(po, wb["x0"], wb["obs"], wb["n_obs"])
     # up to 10 re-linearisations carry the last-bit differences of each QP into the next linearisation
-    # point: measured 2.0e-9 on one elastic C3 instance, <= 2.5e-10 on the hard (status 0) ones
-    check_vs_oracle(r, ro, label=f"SQP {cfg} K={nsqp}", tol=1e-8)
+    # point: measured 3.5e-9 (C3) and 2.0e-9 (C4) on elastic instances, <= 9e-11 on the hard (status 0)
+    # ones; the N = 30 rollout of the C4 one's U moves Xpred by 2.9e-8
+    check_vs_oracle(r, ro, label=f"SQP {cfg} K={nsqp}", tol=1e-8, xtol=1e-7)
     assert (r["iters"] >= 0).all()
 
 
