@@ -27,6 +27,7 @@
 
 #include "../../include/mpcqp.h"
 #include "host_table.h"
+#include "cpu_backend.h"
 
 #define WAVE 64
 #ifndef MPC_NO_NT20
@@ -1053,7 +1054,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                  const int* __restrict__ nobsg, const double* __restrict__ ubarg, double* __restrict__ u0g,
                  double* __restrict__ Ug, double* __restrict__ Xg, int* __restrict__ statusg,
                  int* __restrict__ itersg, int* __restrict__ wlist, int* __restrict__ wcount,
-                 double* __restrict__ stc) {
+                 double* __restrict__ stc, int* __restrict__ wnext) {
     constexpr int G = WAVE / GL;
     constexpr int NR = OBS ? NROW : NROW - 2;    // soft rows held per lane (6, 7: obstacle rows)
     // the Riccati solves of the horizon-specialised kernels are fully unrolled, obstacle kernels included.
@@ -1070,6 +1071,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     int b;
     bool bvalid;
     int cslot = 0;      // MODE_IPM: work-list slot whose record this group uses (a spare group repeats the last)
+    // MODE_XO of an eager call zeroes the other of the context's two list counters for the next call
+    // (launch_solve), so no memset launch separates the batches
+    if (MODE == MODE_XO && wnext && blockIdx.x == 0 && threadIdx.x == 0) *wnext = 0;
     if (MODE == MODE_IPM) {
         // instances deferred by the MODE_XO launch; waves past the end of the list exit at once
         const int cnt = *wcount;
@@ -2095,6 +2099,7 @@ static int fail(int code, const std::string& msg) {
 
 struct mpc_ctx {
     int device;
+    mpcqp_cpu::Backend* cpu;    // device = -1: the host backend (cpu_backend.h); no HIP state is created
     mpc_params p;
     DevTable tab;
     double* table_buf;
@@ -2106,9 +2111,13 @@ struct mpc_ctx {
     double *ls, *lst, *lct;
     size_t cap_lookup;
     hipStream_t stream;
-    // work list of the two-phase launch: wl[0] = count, wl[1..cap_wl] = deferred instance ids
+    // work list of the two-phase launch: wl[0], wl[1] = counts of the eager calls (alternating), wl[2] = count
+    // of a call captured into a graph, wl[3..cap_wl + 2] = deferred instance ids
 #define MPC_WORKLIST_CAP (1 << 20)
+#define MPC_WL_HEAD 3
     int* wl;
+    int wl_epoch;       // counter wl[wl_epoch] serves the next eager call; wl[wl_epoch ^ 1] is zeroed by it
+    bool wl_memset;     // MPC_WL_MEMSET=1: reset the count by a memset launch before every call (A/B switch)
     size_t cap_wl;
     bool two_phase;     // MPC_TWO_PHASE=0 in the environment selects the single MODE_FULL launch
     // the work list is reused by every call: a call on a different stream than the previous one
@@ -2212,10 +2221,26 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     if (!X || !U || T < 2 || Tu < 2) return fail(MPC_E_ARG, "trajectory table needs T >= 2, Tu >= 2");
     int rc = check_params(p);
     if (rc) return rc;
+    if (device == -1) {
+        // host backend: the same table build, the solver on host threads (cpu_backend.h)
+        mpcqp_host::HostTable ht;
+        if (!mpcqp_host::build_host_table(X, T, U, Tu, ht)) return fail(MPC_E_ARG, "bad trajectory table");
+        mpc_ctx* c = (mpc_ctx*)std::calloc(1, sizeof(mpc_ctx));
+        if (!c) return fail(MPC_E_ALLOC, "calloc");
+        c->device = -1;
+        c->p = *p;
+        c->cpu = new (std::nothrow) mpcqp_cpu::Backend(std::move(ht));
+        if (!c->cpu) {
+            std::free(c);
+            return fail(MPC_E_ALLOC, "host backend");
+        }
+        *out = c;
+        return MPC_SUCCESS;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
-        return fail(MPC_E_DEVICE, "no HIP device available (libmpcqp has no CPU backend)");
-    if (device < 0 || device >= ndev) return fail(MPC_E_DEVICE, "device index out of range");
+        return fail(MPC_E_DEVICE, "no HIP device available (device = -1 selects the CPU backend)");
+    if (device < 0 || device >= ndev) return fail(MPC_E_DEVICE, "device index out of range (-1 = CPU backend)");
     HIPCHK(hipSetDevice(device), MPC_E_DEVICE);
     mpcqp_host::HostTable ht;      // monotone s fix, interp columns, global line, bucket index (host_table.h)
     if (!mpcqp_host::build_host_table(X, T, U, Tu, ht)) return fail(MPC_E_ARG, "bad trajectory table");
@@ -2230,6 +2255,8 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         c->two_phase = !(e && e[0] == '0');
         const char* e2 = std::getenv("MPC_STAGE_CACHE");
         c->use_stc = e2 && e2[0] == '1';
+        const char* e3 = std::getenv("MPC_WL_MEMSET");
+        c->wl_memset = e3 && e3[0] == '1';
     }
     if (hipMalloc(&c->table_buf, h.size() * sizeof(double)) != hipSuccess) {
         std::free(c);
@@ -2265,7 +2292,8 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     }
     // work list of the two-phase launch (count + ids), allocated here once so that no solve call
     // allocates; without it every batch runs the single-kernel path
-    if (hipMalloc(&c->wl, sizeof(int) * ((size_t)MPC_WORKLIST_CAP + 1)) == hipSuccess &&
+    if (hipMalloc(&c->wl, sizeof(int) * ((size_t)MPC_WORKLIST_CAP + MPC_WL_HEAD)) == hipSuccess &&
+        hipMemset(c->wl, 0, sizeof(int) * MPC_WL_HEAD) == hipSuccess &&
         hipEventCreateWithFlags(&c->wl_done, hipEventDisableTiming) == hipSuccess) {
         c->cap_wl = MPC_WORKLIST_CAP;
     } else {
@@ -2302,6 +2330,11 @@ static void free_staging(mpc_ctx* c) {
 
 extern "C" void mpc_destroy(mpc_ctx* c) {
     if (!c) return;
+    if (c->cpu) {
+        delete c->cpu;
+        std::free(c);
+        return;
+    }
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     free_staging(c);
@@ -2337,8 +2370,9 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     // The list is allocated once by mpc_create (MPC_WORKLIST_CAP ids), so this path allocates nothing
     // and stays graph-capturable; a larger batch runs the single-kernel path (same results).
     const bool split = kp.polish >= 2 && kp.sqp_iters == 1 && c->two_phase && G >= 2 && (size_t)B <= c->cap_wl;
-    int* wl = split ? c->wl + 1 : nullptr;
-    int* wcnt = split ? c->wl : nullptr;
+    int* wl = split ? c->wl + MPC_WL_HEAD : nullptr;
+    int* wcnt = nullptr;
+    int* wnext = nullptr;
     // Under stream capture (a HIP graph being recorded) the cross-call ordering below is left out: waiting
     // on wl_done, recorded outside the capture, would be a cross-capture dependency that invalidates the
     // capture, and an event recorded inside it belongs to the graph.  Replays of a captured graph are
@@ -2361,14 +2395,24 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
             else { c->stc = nullptr; (void)hipGetLastError(); }
         }
         if (c->use_stc && need <= c->cap_stc) stc = c->stc;
-        // reset by a memset on the stream (not by the kernels): a captured graph replays correctly
-        HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
+        if (capturing || c->wl_memset) {
+            // a captured call resets its own count by a memset inside the graph, so every replay starts
+            // from zero (an eager call's reset would not be replayed)
+            wcnt = capturing ? c->wl + 2 : c->wl + c->wl_epoch;
+            HIPCHK(hipMemsetAsync(wcnt, 0, sizeof(int), st), MPC_E_DEVICE);
+        } else {
+            // eager calls alternate between two counts: this call's MODE_XO zeroes the other one, which the
+            // next call (same stream, or ordered after this one by wl_done) uses; no memset launch
+            wcnt = c->wl + c->wl_epoch;
+            wnext = c->wl + (c->wl_epoch ^ 1);
+        }
     }
     // obstacle rows exist only when obstacles are passed
 #define MPC_LAUNCH(GLV, OBSV, MODEV, NTV)                                                                   \
     hipLaunchKernelGGL((mpc_solve_kernel<GLV, OBSV, MODEV, NTV>), grid, dim3(WAVE),                    \
                        MODEV == MODE_XO ? lds_lite : lds_wave, st, c->tab, kp, B,                           \
-                       x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt, stc)
+                       x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt, stc,                 \
+                       MODEV == MODE_XO ? wnext : nullptr)
     // horizon-specialised kernels for the BASELINE horizons (N = 20: C2, C3; N = 30: C4; N = 40: C5), whose
     // unrolled recursions pay for their code size (C4 0.89 -> 0.66 ms, C5 5.67 -> 4.16 ms)
 #define MPC_LAUNCH_GL(MODEV)                                                                   \
@@ -2384,6 +2428,8 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
     if (split) {
         MPC_LAUNCH_GL(MODE_XO);
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
+        // the launched MODE_XO zeroed wl[epoch ^ 1] and uses wl[epoch]: the next eager call takes the other
+        if (wnext) c->wl_epoch ^= 1;
         MPC_LAUNCH_GL(MODE_IPM);
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
         if (!capturing) {
@@ -2412,10 +2458,15 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
     if (c->p.max_obs > 0 && n_obs && !obs) return fail(MPC_E_ARG, "n_obs given but obs is NULL");
     if (obs && c->p.max_obs == 0)
         return fail(MPC_E_ARG, "obs given but params.max_obs == 0 (the obstacles would be ignored)");
-    if (((uintptr_t)u0 | (uintptr_t)U) & 15)
-        return fail(MPC_E_ARG, "u0 and U must be 16-byte aligned (hipMalloc and torch allocations are)");
     int rc = check_params(&c->p);
     if (rc) return rc;
+    if (c->cpu) {
+        // host context: the pointers are host memory and the call is synchronous (stream ignored)
+        c->cpu->solve_batch(c->p, B, x0, obs, n_obs, ubar, u0, U, Xpred, status, iters);
+        return MPC_SUCCESS;
+    }
+    if (((uintptr_t)u0 | (uintptr_t)U) & 15)
+        return fail(MPC_E_ARG, "u0 and U must be 16-byte aligned (hipMalloc and torch allocations are)");
     KParams kp = kparams(&c->p);
     if (!obs) kp.max_obs = 0;
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
@@ -2438,9 +2489,13 @@ extern "C" int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double
     if (!x0) return fail(MPC_E_ARG, "x0 is NULL");
     int rc = check_params(&c->p);
     if (rc) return rc;
-    HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
     const int N = c->p.N, mo = c->p.max_obs;
     if (obs && mo == 0) return fail(MPC_E_ARG, "obs given but params.max_obs == 0 (the obstacles would be ignored)");
+    if (c->cpu) {
+        c->cpu->solve_batch(c->p, B, x0, mo > 0 ? obs : nullptr, n_obs, ubar, u0, U, Xpred, status, iters);
+        return MPC_SUCCESS;
+    }
+    HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
     if ((size_t)B > c->cap_B || N > c->cap_N || mo > c->cap_obs) {
         size_t nb = (size_t)B > c->cap_B ? (size_t)B : c->cap_B;
         int nn = N > c->cap_N ? N : c->cap_N;
@@ -2499,6 +2554,9 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
     mpc_fsm F;
     if (fsm) F = *fsm; else mpc_default_fsm(&F);     // NULL: both scenarios off
     const bool with_fsm = fsm && (F.dynamic_obstacle || F.traffic_light);
+    if (c->cpu)
+        return c->cpu->closed_loop(c->p, B, x_init, F, with_fsm, max_steps, s_stop, hist_x, hist_u, hist_obs_s,
+                                   hist_tl, hist_status, n_steps, step_ms);
     KParams kp = kparams(&c->p);
     kp.max_obs = with_fsm ? 2 : 0;          // the FSM yields at most the car and the light
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
@@ -2648,6 +2706,10 @@ extern "C" int mpc_global_pose(mpc_ctx* c, int n, const double* s, const double*
     if (!c) return fail(MPC_E_ARG, "ctx is NULL");
     if (n < 0 || (n > 0 && (!s || !d || !out))) return fail(MPC_E_ARG, "bad global-pose arguments");
     if (n == 0) return MPC_SUCCESS;
+    if (c->cpu) {
+        c->cpu->pose(n, s, d, out);
+        return MPC_SUCCESS;
+    }
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
     double* buf = nullptr;
     HIPCHK(hipMalloc(&buf, sizeof(double) * 5 * (size_t)n), MPC_E_ALLOC);
@@ -2710,6 +2772,10 @@ extern "C" int mpc_lookup(mpc_ctx* c, int n, const double* s, double* out_state,
     if (!c) return fail(MPC_E_ARG, "ctx is NULL");
     if (n < 0 || (n > 0 && !s)) return fail(MPC_E_ARG, "bad lookup arguments");
     if (n == 0) return MPC_SUCCESS;
+    if (c->cpu) {
+        c->cpu->lookup(n, s, out_state, out_control);
+        return MPC_SUCCESS;
+    }
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
     if ((size_t)n > c->cap_lookup) {
         if (grow(&c->ls, n) || grow(&c->lst, (size_t)n * 5) || grow(&c->lct, (size_t)n * 2))
