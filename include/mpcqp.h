@@ -15,8 +15,10 @@
  *   - per-instance solver outcomes go to status[] and never fail the call
  *     (the reference ignores SLSQP's status, trajectory_tracking.py:260-263);
  *   - API misuse returns a negative MPC_E* code and sets mpc_last_error();
- *   - a context is bound to one HIP device and is not re-entrant.
- *   - There is no CPU backend: mpc_create fails loudly (MPC_E_DEVICE) without a GPU.
+ *   - a context is bound to one HIP device, or to the host backend (device = -1), and is not re-entrant.
+ *   - Without a GPU, mpc_create with a device index >= 0 fails loudly (MPC_E_DEVICE); device = -1 selects the
+ *     host (CPU) backend explicitly (BASELINE config 1, the reference's CPU path): the same solver, outputs
+ *     and status codes on host threads (csrc/cpu_backend.h; MPC_CPU_THREADS sets the thread count).
  */
 #ifndef MPCQP_H
 #define MPCQP_H
@@ -83,7 +85,8 @@ typedef struct mpc_ctx mpc_ctx;
 /* Fill p with the reference values of trajectory_tracking.py:17-47 (N=5) and solver defaults. */
 void mpc_default_params(mpc_params* p);
 
-/* Create a context on HIP device `device`.  X: T x 5 reference states (s,d,o,k,v), U: Tu x 2
+/* Create a context on HIP device `device` (>= 0), or on the host backend (device = -1).
+ * X: T x 5 reference states (s,d,o,k,v), U: Tu x 2
  * reference controls, exactly the arrays of the trajectory JSON (trajectory_loader.py:22-24);
  * the strict-monotone s fix of trajectory_loader.py:26-30 is applied here.  The table is copied
  * to device memory (owned by the context).  Replaces TrajectoryLoader(...) + TrajectoryTracker(X_ref). */
@@ -103,6 +106,7 @@ int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, cons
                     const double* ubar, double* u0, double* U, double* Xpred, int* status, int* iters);
 
 /* Same, with device pointers, launched asynchronously on `stream` (a hipStream_t; 0 = null stream).
+ * On a host context (device = -1) the pointers are host memory and the call is synchronous.
  * Same argument contract as mpc_solve_batch (n_obs NULL = all max_obs rows; obs with max_obs == 0 is
  * MPC_E_ARG); u0 and U must be 16-byte aligned (they are written with 16-byte stores).  No host synchronisation and, once warmed up, no allocation (graph-capturable): the
  * two-phase work list is allocated by mpc_create for up to 2^20 instances (a larger B runs the

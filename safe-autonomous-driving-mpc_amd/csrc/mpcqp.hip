@@ -66,6 +66,8 @@ struct KParams {
     double w_d, w_o, w_v, w_u1, w_u2;
     double osd, tgap, L, sl, brake_distance, brake_accel;
     double tol, tol_mu, rho, sqp_tol;
+    int dbg;           // diagnostics only (MPC_DBG, default 0): 1 = the crossover kernel defers without the
+                       // work-list atomic (timing probe; the interior-point launch then sees an empty list)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1871,8 +1873,12 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         // S.Xr its rollout (a failed crossover leaves no state behind), which the stage cache keeps
         int slot = 0;
         if (bvalid && gl == 0) {
-            slot = atomicAdd(wcount, 1);
-            wlist[slot] = b;
+            if (Pr.dbg & 1) {
+                slot = b;
+            } else {
+                slot = atomicAdd(wcount, 1);
+                wlist[slot] = b;
+            }
         }
         slot = __shfl(slot, grp2 * GL, WAVE);
         if (bvalid && stc) {
@@ -2211,6 +2217,8 @@ static KParams kparams(const mpc_params* p) {
     k.rho = p->elastic_rho;
     k.polish = p->polish;
     k.sqp_tol = p->sqp_tol;
+    const char* dbg = std::getenv("MPC_DBG");
+    k.dbg = dbg ? std::atoi(dbg) : 0;
     return k;
 }
 
@@ -2221,6 +2229,7 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
     if (!X || !U || T < 2 || Tu < 2) return fail(MPC_E_ARG, "trajectory table needs T >= 2, Tu >= 2");
     int rc = check_params(p);
     if (rc) return rc;
+    if (device < -1) return fail(MPC_E_DEVICE, "device index out of range (-1 = CPU backend)");
     if (device == -1) {
         // host backend: the same table build, the solver on host threads (cpu_backend.h)
         mpcqp_host::HostTable ht;

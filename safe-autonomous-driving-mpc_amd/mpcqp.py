@@ -1,8 +1,9 @@
 """ctypes binding of libmpcqp.so (include/mpcqp.h) — the MI355X batched tracking-MPC solver.
 
 This is the product's host boundary.  It loads the in-tree HIP library and fails loudly when
-it is missing or when no GPU is present: there is no CPU fallback (the CPU restatement in
-oracle/ is test infrastructure and is never used here).
+it is missing or when a GPU context is asked for without a GPU: nothing falls back silently.  device=-1
+selects the library's host backend explicitly (csrc/cpu_backend.h; BASELINE config 1's CPU path).  The
+CPU restatement in oracle/ is test infrastructure and is never used here.
 """
 import ctypes as C
 import os

@@ -17,8 +17,9 @@ about its solution until U moves by at most `sqp_tol` (at most `sqp_iters` QPs; 
 and after 5 elastic QPs in a row, include/mpcqp.h).  By default solve()
 therefore returns the optimum of the reference's own nonlinear problem (pinned to it by
 tests/golden/nlp_golden.npz), which its SLSQP only approximates; `sqp_iters = 1` gives the single
-tracking QP at the warm start that bench.py times.  There is no CPU fallback: without libmpcqp.so or a
-GPU, solve() raises.
+tracking QP at the warm start that bench.py times.  Nothing falls back silently: without libmpcqp.so, or
+without a GPU for a device index, solve() raises; TrajectoryTracker(X_ref, device=-1) runs the library's host
+backend (config 1's CPU path).
 """
 import time
 

@@ -4,10 +4,11 @@ tests/asan/Makefile builds, with -fsanitize=address,undefined (every report fata
   json_driver    csrc/host_table.h -- the native trajectory JSON reader (replaces the json.load of
                  trajectory_loader.py:13-24), the device-table build (:26-84) and the bucketed interval
                  search restated from the device's seg_t;
-  oracle_driver  oracle/mpc_oracle.c -- the CPU restatement.
+  oracle_driver  oracle/mpc_oracle.c -- the CPU restatement;
+  cpu_driver     csrc/cpu_backend.h -- the product's host backend (mpc_create device = -1), on 3 threads.
 The reader runs over the reference trajectories (regenerated from the package data, verbatim floats) and a
 malformed / duplicate-key / deeply nested corpus; every answer must match Python's json.load (the
-reference's loader).  The oracle driver's results must equal the regular build's bit for bit.
+reference's loader).  Both solver drivers' results must equal the regular oracle build's bit for bit.
 """
 import json
 import os
@@ -31,7 +32,7 @@ def drivers():
     with FileLock(os.path.join(ASAN, ".build.lock")):
         r = subprocess.run(["make", "-C", ASAN], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    return os.path.join(ASAN, "json_driver"), os.path.join(ASAN, "oracle_driver")
+    return os.path.join(ASAN, "json_driver"), os.path.join(ASAN, "oracle_driver"), os.path.join(ASAN, "cpu_driver")
 
 
 def traj_json(i):
@@ -135,8 +136,12 @@ def _oracle_inputs(B, kind, seed):
     return X, U, wb["x0"], obs, nob.astype(np.int32), mo, wb["traj"], wb["N"]
 
 
+@pytest.mark.parametrize("drv", [1, 2], ids=["oracle", "cpu_backend"])
 @pytest.mark.parametrize("kind,B,sqp", [(0, 48, 1), ("fsm", 32, 10), (8, 12, 1)])
-def test_oracle_under_asan_matches_regular_build(drivers, tmp_path, kind, B, sqp):
+def test_oracle_under_asan_matches_regular_build(drivers, tmp_path, kind, B, sqp, drv):
+    """The oracle (drv 1) and the product's host backend (drv 2, csrc/cpu_backend.h on 3 threads), both built
+    with ASan/UBSan, against the regular oracle build: bit-identical (the backend performs the oracle's sequence
+    of IEEE operations)."""
     import oracle as O
     X, U, x0, obs, nob, mo, ti, N = _oracle_inputs(B, kind, 5)
     fin = tmp_path / "in.bin"
@@ -146,7 +151,7 @@ def test_oracle_under_asan_matches_regular_build(drivers, tmp_path, kind, B, sqp
             f.write(np.ascontiguousarray(a, np.float64).tobytes())
         f.write(np.ascontiguousarray(nob, np.int32).tobytes())
     fout = tmp_path / "out.bin"
-    r = subprocess.run([drivers[1], str(fin), str(fout)], capture_output=True, text=True, env=ENV, timeout=600)
+    r = subprocess.run([drivers[drv], str(fin), str(fout)], capture_output=True, text=True, env=ENV, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "runtime error" not in r.stderr, r.stderr[-3000:]
     raw = fout.read_bytes()

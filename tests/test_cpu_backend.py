@@ -1,0 +1,165 @@
+"""The host backend of the C ABI: mpc_create(..., device = -1, ...) (csrc/cpu_backend.h).
+
+BASELINE config 1 is the reference's tracker on the CPU ("trajectory1.json, N=10, single ego, CPU path").
+These tests run here, without a GPU, through libmpcqp.so's own entry points and the shim:
+  - batched solves of every config shape (single QP and the drop-in SQP) against the oracle, to 1e-12 with
+    identical status and iteration counts (the backend performs the oracle's sequence of IEEE operations; it
+    is a separate implementation in the product library, and the oracle is only the checker here);
+  - lookups and global poses against the reference goldens (interp_golden bit-exact, pose_golden);
+  - the device-pointer entry on a host context (host pointers, synchronous);
+  - config 1 end to end: mpc_closed_loop on the host equals the shim's run_simulation loop over the same
+    backend bit for bit and runs the reference's 172 steps (+-2); the trajectory2 FSM scenario from the reference
+    start runs the reference's 985 steps, its FSM histories equal the golden-pinned host FSM on its states,
+    and the restated checks pass.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import load_golden, traj_arrays
+
+CFG_B = {"C1": 1, "C2": 512, "C3": 512, "C4": 256, "C5": 128}
+
+
+@pytest.fixture(scope="module")
+def env():
+    import __graft_entry__ as g
+    g.build()
+    import mpcqp
+    import oracle as O
+    import trajectory_tracking as TT
+    import workloads as W
+    from trajectory_loader import TrajectoryLoader, builtin_trajectory
+    return mpcqp, O, TT, W, TrajectoryLoader, builtin_trajectory
+
+
+def test_create_selects_backend(env):
+    """device = -1 creates a host context without any GPU; an out-of-range device fails loudly."""
+    mpcqp = env[0]
+    X, U = traj_arrays(1)
+    p = mpcqp.default_params(N=10)
+    slv = mpcqp.Solver(X, U, p, device=-1)
+    r = slv.solve_batch(np.array([[1.0, 0.0, 0.0, 0.0, 1.0]]))
+    assert np.isfinite(r["U"]).all() and r["status"][0] == 0
+    h = ctypes.c_void_p()
+    rc = mpcqp.lib().mpc_create(mpcqp._p(np.ascontiguousarray(X)), X.shape[0], mpcqp._p(np.ascontiguousarray(U)),
+                                U.shape[0], ctypes.byref(p), -2, ctypes.byref(h))
+    assert rc == -2 and "device index" in mpcqp.last_error()
+
+
+@pytest.mark.parametrize("sqp", [1, 30])
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4", "C5"])
+def test_backend_equals_oracle(env, cfg, sqp):
+    mpcqp, O, _, W, _, _ = env
+    w = W.make_batch(cfg)
+    B = CFG_B[cfg]
+    x0 = w["x0"][:B]
+    obs = None if w["obs"] is None else w["obs"][:B]
+    nob = None if w["n_obs"] is None else w["n_obs"][:B]
+    ld = W.loader(w["traj"])
+    p = mpcqp.default_params(N=w["N"], max_obs=w["max_obs"], sqp_iters=sqp)
+    r = mpcqp.Solver(ld.X_ref, ld.U_ref, p, device=-1).solve_batch(x0, obs, nob)
+    ro = O.Oracle(ld.X_ref, ld.U_ref).solve_batch(O.default_params(N=w["N"], max_obs=w["max_obs"], sqp_iters=sqp),
+                                                  x0, obs, nob)
+    err = float(np.abs(r["U"] - ro["U"]).max())
+    print(f"{cfg} sqp_iters={sqp} B={B}: max|dU| {err:.1e}, bit-identical {np.array_equal(r['U'], ro['U'])}")
+    assert err <= 1e-12
+    assert np.abs(r["Xpred"] - ro["Xpred"]).max() <= 1e-10
+    assert np.array_equal(r["u0"], r["U"][:, 0])
+    assert np.array_equal(r["status"], ro["status"]) and np.array_equal(r["iters"], ro["iters"])
+
+
+@pytest.mark.parametrize("ti", [1, 2, 3])
+def test_lookup_and_pose_match_goldens(env, ti):
+    mpcqp = env[0]
+    slv = mpcqp.Solver(*traj_arrays(ti), mpcqp.default_params(), device=-1)
+    g = load_golden("interp_golden")
+    st, ct = slv.lookup(g[f"t{ti}_s"])
+    assert np.array_equal(st, g[f"t{ti}_state"]) and np.array_equal(ct, g[f"t{ti}_control"])
+    gp = load_golden("pose_golden")
+    P = slv.global_pose(gp[f"t{ti}_s"], gp[f"t{ti}_d"])
+    assert np.abs(P - gp[f"t{ti}_pose"]).max() <= 1e-9
+
+
+def test_device_entry_on_host_context(env):
+    """mpc_solve_batch_device with a host context takes host pointers and runs synchronously."""
+    mpcqp, _, _, W, _, _ = env
+    w = W.make_batch("C3", B=64)
+    ld = W.loader(w["traj"])
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=20, max_obs=2), device=-1)
+    ref = slv.solve_batch(w["x0"], w["obs"], w["n_obs"])
+    B = 64
+    x0 = np.ascontiguousarray(w["x0"])
+    obs = np.ascontiguousarray(w["obs"])
+    nob = np.ascontiguousarray(w["n_obs"], np.int32)
+    u0 = np.zeros((B, 2)); U = np.zeros((B, 20, 2)); X = np.zeros((B, 21, 5))
+    st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
+    a = lambda v: v.ctypes.data
+    slv.solve_batch_device(B, a(x0), a(obs), a(nob), None, a(u0), a(U), a(X), a(st), a(it), 0)
+    assert np.array_equal(U, ref["U"]) and np.array_equal(X, ref["Xpred"]) and np.array_equal(st, ref["status"])
+
+
+def _host_loop(TT, mpc, fsm, traj, x0, max_steps):
+    """The shim's run_simulation body from a given start (the solver is the context's: here the host one)."""
+    x = np.asarray(x0, np.float64)
+    hx, hu, ho, ht = [x], [], [], []
+    while x[0] <= traj.s_max - 1.0 and len(hu) < max_steps:
+        obstacles, tl = fsm.update(mpc.dt, x[0], x[4])
+        u, _, _ = mpc.solve(x, obstacles)
+        x = x + mpc.dt * mpc.dynamics(x, u, traj.get_state(x[0])[3])
+        hx.append(x)
+        hu.append(u)
+        car = [o["s"] for o in obstacles if o["type"] == "car"]
+        ho.append(car[0] if car else np.nan)
+        ht.append(1 if tl == "GREEN" else 0)
+    return np.array(hx), np.array(hu), np.array(ho), np.array(ht)
+
+
+def test_config1_closed_loop(env):
+    """Config 1 (traj1, N=10, no obstacles, the reference start [0,0,0,0,0.5]) on the host backend: the
+    batched closed loop equals the shim loop bit for bit and runs the reference's 172 steps (+-2)."""
+    _, _, TT, _, TL, bt = env
+    traj = TL(bt(1))
+    mpc = TT.TrajectoryTracker(traj, device=-1)
+    mpc.N = 10
+    x_init = np.array([[0.0, 0.0, 0.0, 0.0, 0.5], [1.0, 0.05, 0.0, 0.0, 1.5]])
+    r = TT.run_simulation_batch(mpc, TT.ObstaclesFSM(), traj, x_init=x_init, max_steps=600, checks=True)
+    for b in range(2):
+        hx, hu, _, ht = _host_loop(TT, mpc, TT.ObstaclesFSM(), traj, x_init[b], 600)
+        n = int(r["n_steps"][b])
+        assert n == len(hu)
+        assert np.array_equal(r["hist_x"][b, :n + 1], hx) and np.array_equal(r["hist_u"][b, :n], hu)
+        assert np.array_equal(r["hist_tl"][b, :n], ht)
+    g = load_golden("closedloop_golden")
+    # the reference's SLSQP (ftol 1e-3) and the exact NLP optimum brake a step apart: steps within +-2
+    assert abs(int(r["n_steps"][0]) - len(g["c1_traj1_N10_hist_u"])) <= 2
+    m = min(int(r["n_steps"][0]), len(g["c1_traj1_N10_hist_u"])) + 1
+    assert np.abs(r["hist_x"][0, :m, 1] - g["c1_traj1_N10_hist_x"][:m, 1]).max() < 0.1
+    assert r["checks_passed"].all()
+
+
+def test_traj2_fsm_closed_loop_vs_reference_run(env):
+    """The reference scenario (trajectory2 FSM preset :292-308, N = 5, reference start) on the host backend."""
+    _, _, TT, _, TL, bt = env
+    traj = TL(bt(2))
+    mpc = TT.TrajectoryTracker(traj, device=-1)
+    mpc.N = 5
+    fsm = TT.ObstaclesFSM(dynamic_obstacle=True, traffic_light=True)
+    r = TT.run_simulation_batch(mpc, fsm, traj, max_steps=3000, checks=True)
+    g = load_golden("closedloop_golden")
+    n = int(r["n_steps"][0])
+    assert abs(n - len(g["traj2_N5_fsm_hist_u"])) <= 2
+    assert r["checks_passed"][0]
+    hx = r["hist_x"][0, :n + 1]
+    f = TT.ObstaclesFSM(dynamic_obstacle=True, traffic_light=True)
+    obs_s, tl = [], []
+    for k in range(n):
+        obstacles, state = f.update(mpc.dt, hx[k, 0], hx[k, 4])
+        car = [o["s"] for o in obstacles if o["type"] == "car"]
+        obs_s.append(car[0] if car else np.nan)
+        tl.append(1 if state == "GREEN" else 0)
+    obs_s = np.array(obs_s)
+    ho = r["hist_obs_s"][0, :n]
+    assert np.array_equal(np.isnan(ho), np.isnan(obs_s)) and np.array_equal(ho[~np.isnan(ho)], obs_s[~np.isnan(obs_s)])
+    assert np.array_equal(r["hist_tl"][0, :n], np.array(tl))
