@@ -207,6 +207,7 @@ def main():
             out["closed_loop"] = cl
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
+            out["cpu_backend"] = cpu_backend(wb, N, mo, min(args.cpu_seconds, 5.0))
             out["cpu_reference"] = cpu_reference(wb, N, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -385,6 +386,31 @@ def cpu_baseline(wb, N, mo, budget_s):
     return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port", "host": hw,
             "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by the oracle's C PDIP "
                       f"(oracle/mpc_oracle.c) with OpenMP, {threads} threads"}
+
+
+def cpu_backend(wb, N, mo, budget_s):
+    """The product's own host backend (libmpcqp, mpc_create device = -1: csrc/cpu_backend.h) on the same bounded
+    sample and CPU share as cpu_baseline: what a user without a GPU gets (config 1's CPU path)."""
+    import mpcqp
+    import workloads as W
+    ld = W.loader(wb["traj"])
+    hw = host_cores()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hw["affinity_cpus"]
+    os.environ["MPC_CPU_THREADS"] = str(threads)
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo), device=-1)
+    n = min(512, wb["x0"].shape[0])
+    sl = slice(0, n)
+    obs = None if wb["obs"] is None else wb["obs"][sl]
+    nob = None if wb["n_obs"] is None else wb["n_obs"][sl]
+    slv.solve_batch(wb["x0"][sl], obs, nob)          # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        slv.solve_batch(wb["x0"][sl], obs, nob)
+        done += n
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "solves/s", "cores": threads,
+            "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by libmpcqp's host "
+                      f"backend (device = -1), {threads} threads"}
 
 
 def host_cores():
