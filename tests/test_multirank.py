@@ -1,6 +1,7 @@
 """Multi-rank path on CPU (gloo, world_size 2): contiguous ego shards, no data-path exchange, one
-telemetry gather at the end.  The per-rank solver here is the CPU oracle, standing in
-for libmpcqp (which needs a GPU); what is under test is the partition and the collective."""
+telemetry gather at the end.  The per-rank solver is libmpcqp itself on its host backend
+(mpc_create device = -1: the same entries, solver and closed loop as on the GPU); what is under test is the
+partition and the collective, run through the product's code path."""
 import os
 import socket
 
@@ -25,15 +26,15 @@ def _rank_main(rank, world, port, total, outdir):
     sys.path[:0] = [here, root, os.path.join(root, "safe-autonomous-driving-mpc_amd"), os.path.join(root, "oracle")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
-    import oracle as O
+    import mpcqp
     import shard
     import workloads as W
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard.shard_range(total, world, rank)
     wb = W.make_batch("C3", B=hi - lo, offset=lo)
-    orc = O.Oracle(*traj_arrays(wb["traj"]))
-    r = orc.solve_batch(O.default_params(N=wb["N"], max_obs=wb["max_obs"]), wb["x0"], wb["obs"], wb["n_obs"],
-                        num_threads=1)
+    os.environ["MPC_CPU_THREADS"] = "1"
+    slv = mpcqp.Solver(*traj_arrays(wb["traj"]), mpcqp.default_params(N=wb["N"], max_obs=wb["max_obs"]), device=-1)
+    r = slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
     mat = shard.gather_telemetry(shard.telemetry(r["status"], r["iters"]))
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), U=r["U"], status=r["status"], iters=r["iters"], mat=mat,
              lo=lo, hi=hi)
@@ -59,18 +60,23 @@ def test_make_batch_offset_is_a_slice_of_the_stream():
     assert np.array_equal(part["obs"], full["obs"][20:35])
 
 
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    import __graft_entry__ as g
+    g.build()
+
+
 def test_two_rank_gloo_matches_single_process(tmp_path):
     import torch.multiprocessing as mp
-    import oracle as O
+    import mpcqp
     import shard
     import workloads as W
     total = 96
     mp.spawn(_rank_main, args=(WORLD, _free_port(), total, str(tmp_path)), nprocs=WORLD, join=True)
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(WORLD)]
     wb = W.make_batch("C3", B=total)
-    orc = O.Oracle(*traj_arrays(wb["traj"]))
-    ref = orc.solve_batch(O.default_params(N=wb["N"], max_obs=wb["max_obs"]), wb["x0"], wb["obs"], wb["n_obs"],
-                          num_threads=1)
+    slv = mpcqp.Solver(*traj_arrays(wb["traj"]), mpcqp.default_params(N=wb["N"], max_obs=wb["max_obs"]), device=-1)
+    ref = slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"])
     U = np.concatenate([p["U"] for p in parts])
     assert np.array_equal(U, ref["U"])                       # shards are independent: bit-identical
     # every rank holds the same gathered telemetry, and it sums to the single-process batch
@@ -98,35 +104,18 @@ def cl_inputs(total):
 
 
 def cpu_closed_loop(x_init, max_steps, N=5):
-    """CPU stand-in for mpcqp.Solver.closed_loop (same result layout): the shim's FSM and plant with the
-    oracle's solve; every step is charged 1 ms (deterministic quantities)."""
-    import oracle as O
+    """mpcqp.Solver.closed_loop on libmpcqp's host backend (device = -1): the closed-loop entry bench.py's
+    --closed-loop leg calls, with the trajectory2 FSM and the drop-in SQP default.  Step times are replaced
+    by 1 ms so that the check quantities are deterministic."""
+    import mpcqp
     import trajectory_tracking as TT
     from trajectory_loader import TrajectoryLoader, builtin_trajectory
     traj = TrajectoryLoader(builtin_trajectory(2))
-    orc = O.Oracle(traj.X_ref, traj.U_ref)
-    B = x_init.shape[0]
-    r = dict(hist_x=np.full((B, max_steps + 1, 5), np.nan), hist_u=np.full((B, max_steps, 2), np.nan),
-             hist_obs_s=np.full((B, max_steps), np.nan), hist_tl=np.full((B, max_steps), -1, np.int32),
-             n_steps=np.zeros(B, np.int32), step_ms=np.ones(max_steps))
-    mpc = TT.TrajectoryTracker(traj)
-    for b in range(B):
-        fsm = TT.ObstaclesFSM(True, True)
-        x = x_init[b].copy()
-        r["hist_x"][b, 0] = x
-        n = 0
-        while x[0] <= traj.s_max - 1.0 and n < max_steps:
-            obstacles, tl = fsm.update(0.2, x[0], x[4])
-            ob = np.array([[o["s"], o["v"]] for o in obstacles]).reshape(-1, 2)
-            res = orc.solve(O.default_params(N=N, max_obs=len(ob), sqp_iters=TT.SQP_ITERS), x, ob if len(ob) else None)
-            x = x + 0.2 * mpc.dynamics(x, res["u0"], traj.get_state(x[0])[3])
-            r["hist_x"][b, n + 1] = x
-            r["hist_u"][b, n] = res["u0"]
-            car = [o["s"] for o in obstacles if o["type"] == "car"]
-            r["hist_obs_s"][b, n] = car[0] if car else np.nan
-            r["hist_tl"][b, n] = 1 if tl == "GREEN" else 0
-            n += 1
-        r["n_steps"][b] = n
+    os.environ["MPC_CPU_THREADS"] = "1"
+    slv = mpcqp.Solver(traj.X_ref, traj.U_ref, mpcqp.default_params(N=N, sqp_iters=TT.SQP_ITERS), device=-1)
+    r = slv.closed_loop(x_init, TT.fsm_params(TT.ObstaclesFSM(True, True)), max_steps=max_steps, s_max=traj.s_max)
+    slv.close()
+    r["step_ms"] = np.ones(max_steps)
     return r, traj
 
 
