@@ -30,9 +30,8 @@
 #define MAXN MPC_MAX_N
 #define NROW 9      /* soft one-sided rows per stage                       */
 #define NBOX 4      /* hard box rows per control stage                     */
-#define XI0 1e-1    /* initial elastic slack                                */
 #define TAU 0.995   /* fraction to the boundary                             */
-#define MU0 1000.0   /* initial complementarity of the soft rows                */
+#define START_SHIFT 3.0   /* interior-point start: slack and elastic slack beyond the row value */
 
 struct orc_table {
     int T, Tu;
@@ -62,7 +61,7 @@ void orc_default_params(mpc_params* p) {
     p->sqp_iters = 1;
     p->max_iter = 80;
     p->tol = 1e-9;
-    p->tol_mu = 1e-9;
+    p->tol_mu = 1e-10;
     p->elastic_rho = 1e5;
     p->polish = 2;
     p->sqp_tol = 1e-10;
@@ -814,43 +813,6 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
     int nsoft = 0;
     for (int j = 0; j < NROW; ++j) nsoft += Q->on[j];
     double Mtot = (double)(2 * nsoft * N + NBOX * N);
-    double bscale = 0.0;
-    for (int k = 1; k <= N; ++k)
-        for (int j = 0; j < NROW; ++j) {
-            if (!Q->on[j]) continue;
-            /* centred start: xi covers the violation, s*lam = MU0 with lam <= rho/2, nu = rho - lam */
-            double r0 = -Q->b[k][j];
-            double xi = (r0 < 0 ? -r0 : 0.0) + XI0;
-            double sv = r0 + xi;
-            double lam = MU0 / sv < 0.5 * rho ? MU0 / sv : 0.5 * rho;
-            S->xi[k][j] = xi;
-            S->s[k][j] = sv;
-            S->lam[k][j] = lam;
-            S->nu[k][j] = rho - lam;
-            if (fabs(Q->b[k][j]) > bscale) bscale = fabs(Q->b[k][j]);
-        }
-    /* box rows start on the rows' central path: sb*lb = the mean soft-row complementarity.  The elastic
-     * rows' products are of order rho (1e5); box multipliers started at 1 need ~8 short-step iterations
-     * to grow to that scale when a violated row pushes a control onto its box. */
-    double rowc = 0.0;
-    for (int k = 1; k <= N; ++k)
-        for (int j = 0; j < NROW; ++j)
-            if (Q->on[j]) rowc += S->s[k][j] * S->lam[k][j] + S->xi[k][j] * S->nu[k][j];
-    const double mrow = rowc / (double)(2 * nsoft * N);
-    for (int t = 0; t < N; ++t)
-        for (int j = 0; j < NBOX; ++j) {
-            double r0 = -Q->bb[t][j];
-            S->sb[t][j] = r0 > 1.0 ? r0 : 1.0;
-            S->lb[t][j] = mrow / S->sb[t][j];
-            if (fabs(Q->bb[t][j]) > bscale) bscale = fabs(Q->bb[t][j]);
-        }
-    double X[MAXN + 1][5];
-    double y[MAXN + 1][5], yc[MAXN + 1][5], ya[MAXN + 1][5], z[MAXN][2], zc[MAXN][2], za[MAXN][2];
-    double rp[MAXN + 1][NROW], rx[MAXN + 1][NROW], rpb[MAXN][NBOX];
-    double r4[MAXN + 1][NROW], r5[MAXN + 1][NROW], r4b[MAXN][NBOX];
-    double gd[2 * MAXN], gc[2 * MAXN], ga[2 * MAXN];
-    int status = MPC_MAX_ITER, it;
-    int stall = 0;
     if (p->polish >= 2) {
         /* Crossover first: the active-set solve started from the unconstrained optimum (all rows
          * inactive, du = 0, multipliers 0), XO_ROUNDS rounds.  When it certifies (KKT-consistent), it is
@@ -865,6 +827,61 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
         }
     }
 
+    double X[MAXN + 1][5];
+    /* Interior-point start (round 3): centred at the unconstrained optimum of QP(ubar) (one Riccati
+     * factorisation and solve without rows).  Each soft row with value r = C x - b there gets slack
+     * max(r, 0) + START_SHIFT and elastic slack max(-r, 0) + START_SHIFT, and the multiplier pair on the
+     * pair's central path with lambda + nu = rho (lambda s = nu xi): primal and dual row residuals are zero
+     * and every pair equally centred.  Box rows start on the rows' central path (sb lb = the mean soft-row
+     * complementarity, sb >= 1).  With tol_mu 1e-10 (round 2: the start at du = 0 with s lam = 1000,
+     * lam <= rho/2, and 1e-9), maximum iterations C2 22 -> 20, C3 24 -> 22, C4 27 -> 25, C5 29 -> 27, and
+     * every feasible C5 instance polish-certified. */
+    {
+        static __thread ipm_fact F0;
+        static __thread ipm_dir D0;
+        double qh[MAXN + 1][5], gh[MAXN][2];
+        for (int k = 1; k <= N; ++k) {
+            memcpy(F0.Qt[k], Q->Q[k], sizeof(F0.Qt[k]));
+            for (int a = 0; a < 5; ++a) qh[k][a] = -Q->q[k][a];
+        }
+        for (int t = 0; t < N; ++t) {
+            F0.Rt[t][0] = Q->R[0];
+            F0.Rt[t][1] = Q->R[1];
+            gh[t][0] = -Q->r[t][0];
+            gh[t][1] = -Q->r[t][1];
+        }
+        riccati_factor(Q, &F0);
+        riccati_solve(Q, &F0, qh, gh, &D0);
+        memcpy(S->du, D0.du, sizeof(double) * 2 * N);
+    }
+    rollout_lin(Q, S->du, X);
+    double bscale = 0.0, rowc = 0.0;
+    for (int k = 1; k <= N; ++k)
+        for (int j = 0; j < NROW; ++j) {
+            if (!Q->on[j]) continue;
+            const double r = dot5(Q->C[j], X[k]) - Q->b[k][j];
+            const double sv = (r > 0.0 ? r : 0.0) + START_SHIFT, xi = (r < 0.0 ? -r : 0.0) + START_SHIFT;
+            S->s[k][j] = sv;
+            S->xi[k][j] = xi;
+            S->lam[k][j] = rho * xi / (sv + xi);
+            S->nu[k][j] = rho * sv / (sv + xi);
+            rowc += sv * S->lam[k][j];
+            if (fabs(Q->b[k][j]) > bscale) bscale = fabs(Q->b[k][j]);
+        }
+    const double mrow = rowc / (double)(nsoft * N);
+    for (int t = 0; t < N; ++t)
+        for (int j = 0; j < NBOX; ++j) {
+            const double v = box_sign[j] * S->du[2 * t + box_comp[j]] - Q->bb[t][j];
+            S->sb[t][j] = v > 1.0 ? v : 1.0;
+            S->lb[t][j] = mrow / S->sb[t][j];
+            if (fabs(Q->bb[t][j]) > bscale) bscale = fabs(Q->bb[t][j]);
+        }
+    double y[MAXN + 1][5], yc[MAXN + 1][5], ya[MAXN + 1][5], z[MAXN][2], zc[MAXN][2], za[MAXN][2];
+    double rp[MAXN + 1][NROW], rx[MAXN + 1][NROW], rpb[MAXN][NBOX];
+    double r4[MAXN + 1][NROW], r5[MAXN + 1][NROW], r4b[MAXN][NBOX];
+    double gd[2 * MAXN], gc[2 * MAXN], ga[2 * MAXN];
+    int status = MPC_MAX_ITER, it;
+    int stall = 0;
     for (it = 0; it < p->max_iter; ++it) {
         rollout_lin(Q, S->du, X);
         memset(yc, 0, sizeof(yc));

@@ -36,9 +36,8 @@ using mpcqp_host::HostTable;
 constexpr int kMaxN = MPC_MAX_N;
 constexpr int kRows = 9;          // soft rows per stage: lane +-d, +-(d + L/2 o), +-(d + L o), 2 obstacle, v >= 0
 constexpr int kBox = 4;           // box rows per control: +u1, -u1, +u2, -u2
-constexpr double kXi0 = 1e-1;     // the device constants (mpcqp.hip: XI0, TAU, MU0, POLISH_*, SQP_*)
-constexpr double kTau = 0.995;
-constexpr double kMu0 = 1000.0;
+constexpr double kTau = 0.995;    // the device constants (mpcqp.hip: TAU, START_SHIFT, POLISH_*, SQP_*)
+constexpr double kStartShift = 3.0;
 constexpr double kDelta = 1e-11;
 constexpr int kRefine = 2;
 constexpr int kPolishRounds = 6;
@@ -691,31 +690,49 @@ private:
         int nsoft = 0;
         for (int j = 0; j < kRows; ++j) nsoft += Q.on[j];
         const double Mtot = (double)(2 * nsoft * N + kBox * N);
+        // start centred at the unconstrained optimum of QP(ubar) (one factorisation and solve without rows):
+        // slack max(r, 0) + shift, elastic slack max(-r, 0) + shift for the row value r there, the multiplier
+        // pair on the pair's central path with lambda + nu = rho; box rows at the mean row complementarity
+        double X[kMaxN + 1][5];
+        {
+            double qh[kMaxN + 1][5], gh[kMaxN][2];
+            for (int k = 1; k <= N; ++k) {
+                std::memcpy(F_.Qt[k], Q.Q[k], sizeof(F_.Qt[k]));
+                for (int a = 0; a < 5; ++a) qh[k][a] = -Q.q[k][a];
+            }
+            for (int t = 0; t < N; ++t) {
+                F_.Rt[t][0] = Q.R[0];
+                F_.Rt[t][1] = Q.R[1];
+                gh[t][0] = -Q.r[t][0];
+                gh[t][1] = -Q.r[t][1];
+            }
+            riccati_factor();
+            riccati_solve(qh, gh, D_);
+            std::memcpy(S_.du, D_.du, sizeof(double) * 2 * N);
+        }
+        rollout(S_.du, X);
         double bscale = 0.0, rowc = 0.0;
         for (int k = 1; k <= N; ++k)
             for (int j = 0; j < kRows; ++j) {
                 if (!Q.on[j]) continue;
-                // centred start: xi covers the violation, s lam = MU0 with lam <= rho/2, nu = rho - lam
-                const double r0 = -Q.b[k][j];
-                const double xi = (r0 < 0 ? -r0 : 0.0) + kXi0;
-                const double sv = r0 + xi;
-                const double lam = std::min(kMu0 / sv, 0.5 * rho);
-                S_.xi[k][j] = xi;
+                const double r = dot5(Q.C[j], X[k]) - Q.b[k][j];
+                const double sv = (r > 0.0 ? r : 0.0) + kStartShift, xi = (r < 0.0 ? -r : 0.0) + kStartShift;
                 S_.s[k][j] = sv;
-                S_.l[k][j] = lam;
-                S_.nu[k][j] = rho - lam;
+                S_.xi[k][j] = xi;
+                S_.l[k][j] = rho * xi / (sv + xi);
+                S_.nu[k][j] = rho * sv / (sv + xi);
+                rowc += sv * S_.l[k][j];
                 bscale = std::max(bscale, std::fabs(Q.b[k][j]));
-                rowc += sv * lam + xi * (rho - lam);
             }
-        const double mrow = rowc / (double)(2 * nsoft * N);
+        const double mrow = rowc / (double)(nsoft * N);
         for (int t = 0; t < N; ++t)
             for (int j = 0; j < kBox; ++j) {
-                const double r0 = -Q.bb[t][j];
-                S_.sb[t][j] = r0 > 1.0 ? r0 : 1.0;
+                const double v = kBoxSign[j] * S_.du[2 * t + kBoxComp[j]] - Q.bb[t][j];
+                S_.sb[t][j] = v > 1.0 ? v : 1.0;
                 S_.lb[t][j] = mrow / S_.sb[t][j];
                 bscale = std::max(bscale, std::fabs(Q.bb[t][j]));
             }
-        double X[kMaxN + 1][5], y[kMaxN + 1][5], yc[kMaxN + 1][5], ya[kMaxN + 1][5];
+        double y[kMaxN + 1][5], yc[kMaxN + 1][5], ya[kMaxN + 1][5];
         double z[kMaxN][2], zc[kMaxN][2], za[kMaxN][2];
         double rp[kMaxN + 1][kRows], rx[kMaxN + 1][kRows], rpb[kMaxN][kBox];
         double r4[kMaxN + 1][kRows], r5[kMaxN + 1][kRows], r4b[kMaxN][kBox];

@@ -69,7 +69,7 @@ class TrajectoryTracker:
         self.max_iter = 80
         self.polish = 2
         self.tol = 1e-9
-        self.tol_mu = 1e-9
+        self.tol_mu = 1e-10
         self.elastic_rho = 1e5
         self.brake_distance = 40.0
         self.brake_accel = -2.0

@@ -44,7 +44,7 @@ int main(int argc, char** argv) {
     p.vehicle_radius = 1.0; p.w_d = 10.0; p.w_o = 10.0; p.w_v = 5.0; p.w_u1 = 0.5; p.w_u2 = 0.5;
     p.obstacle_safety_distance = 5.0; p.max_time_2_obs = 1.5; p.wheelbase = 2.8; p.lane_width = 3.0;
     p.safe_lane_margin = 0.1; p.brake_distance = 40.0; p.brake_accel = -2.0; p.linearization = 1;
-    p.sqp_iters = hdr[5]; p.max_iter = 80; p.tol = 1e-9; p.tol_mu = 1e-9; p.elastic_rho = 1e5; p.polish = 2;
+    p.sqp_iters = hdr[5]; p.max_iter = 80; p.tol = 1e-9; p.tol_mu = 1e-10; p.elastic_rho = 1e5; p.polish = 2;
     p.sqp_tol = 1e-10;
     std::vector<double> Uo((size_t)B * 2 * N), Xo((size_t)B * 5 * (N + 1));
     std::vector<int> st(B), it(B);

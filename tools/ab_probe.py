@@ -29,7 +29,8 @@ def child(lib, cfg, reps, out):
             if wb[k] is not None:
                 wb[k] = wb[k][:B]
     ld = W.loader(wb["traj"])
-    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo))
+    extra = {"sqp_iters": int(os.environ["AB_SQP"])} if os.environ.get("AB_SQP") else {}   # e.g. 30: the SQP leg
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo, **extra))
     dev = torch.device("cuda", 0)
     t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
     x0 = t(wb["x0"])
