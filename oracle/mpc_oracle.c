@@ -829,7 +829,7 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
 
     double X[MAXN + 1][5];
     /* Interior-point start (round 3): centred at the unconstrained optimum of QP(ubar) (one Riccati
-     * factorisation and solve without rows).  Each soft row with value r = C x - b there gets slack
+     * factorisation and solve without rows), or at du = 0 when the soft rows are less violated there.  Each soft row with value r = C x - b there gets slack
      * max(r, 0) + START_SHIFT and elastic slack max(-r, 0) + START_SHIFT, and the multiplier pair on the
      * pair's central path with lambda + nu = rho (lambda s = nu xi): primal and dual row residuals are zero
      * and every pair equally centred.  Box rows start on the rows' central path (sb lb = the mean soft-row
@@ -855,6 +855,22 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
         memcpy(S->du, D0.du, sizeof(double) * 2 * N);
     }
     rollout_lin(Q, S->du, X);
+    {
+        /* the start's primal point: the unconstrained optimum, or du = 0 (the warm start ubar, which already
+         * brakes for obstacles ahead) when the soft rows are less violated there (sum of max(-r, 0)) */
+        double v_unc = 0.0, v_bar = 0.0;
+        for (int k = 1; k <= N; ++k)
+            for (int j = 0; j < NROW; ++j) {
+                if (!Q->on[j]) continue;
+                const double r = dot5(Q->C[j], X[k]) - Q->b[k][j];
+                v_unc += r < 0.0 ? -r : 0.0;
+                v_bar += Q->b[k][j] > 0.0 ? Q->b[k][j] : 0.0;
+            }
+        if (v_bar < v_unc) {
+            memset(S->du, 0, sizeof(double) * 2 * N);
+            rollout_lin(Q, S->du, X);
+        }
+    }
     double bscale = 0.0, rowc = 0.0;
     for (int k = 1; k <= N; ++k)
         for (int j = 0; j < NROW; ++j) {

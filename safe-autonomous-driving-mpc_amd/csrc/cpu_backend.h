@@ -690,7 +690,8 @@ private:
         int nsoft = 0;
         for (int j = 0; j < kRows; ++j) nsoft += Q.on[j];
         const double Mtot = (double)(2 * nsoft * N + kBox * N);
-        // start centred at the unconstrained optimum of QP(ubar) (one factorisation and solve without rows):
+        // start centred at the unconstrained optimum of QP(ubar) (one factorisation and solve without rows), or
+        // at du = 0 when the soft rows are less violated there:
         // slack max(r, 0) + shift, elastic slack max(-r, 0) + shift for the row value r there, the multiplier
         // pair on the pair's central path with lambda + nu = rho; box rows at the mean row complementarity
         double X[kMaxN + 1][5];
@@ -711,6 +712,21 @@ private:
             std::memcpy(S_.du, D_.du, sizeof(double) * 2 * N);
         }
         rollout(S_.du, X);
+        {
+            // primal point: the unconstrained optimum, or du = 0 (ubar) when the soft rows are less violated there
+            double v_unc = 0.0, v_bar = 0.0;
+            for (int k = 1; k <= N; ++k)
+                for (int j = 0; j < kRows; ++j) {
+                    if (!Q.on[j]) continue;
+                    const double r = dot5(Q.C[j], X[k]) - Q.b[k][j];
+                    v_unc += r < 0.0 ? -r : 0.0;
+                    v_bar += Q.b[k][j] > 0.0 ? Q.b[k][j] : 0.0;
+                }
+            if (v_bar < v_unc) {
+                std::memset(S_.du, 0, sizeof(double) * 2 * N);
+                rollout(S_.du, X);
+            }
+        }
         double bscale = 0.0, rowc = 0.0;
         for (int k = 1; k <= N; ++k)
             for (int j = 0; j < kRows; ++j) {

@@ -1287,7 +1287,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         double bad = 0.0;
         if (phase == 1) {
             // Start centred at the unconstrained optimum of QP(ubar) (oracle pdip): one
-            // factorisation and solve without rows gives du and the state x4 of stage k there; each soft row of
+            // factorisation and solve without rows gives du and the state x4 of stage k there (or du = 0, see
+            // below); each soft row of
             // value r gets slack max(r, 0) + START_SHIFT and elastic slack max(-r, 0) + START_SHIFT, and its
             // multiplier pair the pair's central point with lambda + nu = rho; box rows the mean row
             // complementarity.  (Round 2 started at du = 0 with s lam = 1000, lam <= rho / 2 and stopped at
@@ -1315,6 +1316,26 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int a = 0; a < 4; ++a) x4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
             du0 = live ? S.dud[2 * (k - 1)] : 0.0;
             du1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
+            {
+                // primal point: the unconstrained optimum, or du = 0 (the warm start ubar, which already brakes
+                // for obstacles ahead) when the soft rows are less violated there (sum of max(-r, 0))
+                double vu = 0.0, vb = 0.0;
+    #pragma unroll
+                for (int j = 0; j < NR; ++j)
+                    if (ron[j]) {
+                        const double r = rdot(rid<OBS>(j), cf[j], x4) - bk[j];
+                        vu += r < 0.0 ? -r : 0.0;
+                        vb += bk[j] > 0.0 ? bk[j] : 0.0;
+                    }
+                vu = Q.sum(vu);
+                vb = Q.sum(vb);
+                if (vb < vu) {
+    #pragma unroll
+                    for (int a = 0; a < 4; ++a) x4[a] = 0.0;
+                    du0 = 0.0;
+                    du1 = 0.0;
+                }
+            }
             double rowc = 0.0;
     #pragma unroll
             for (int j = 0; j < NR; ++j) {
