@@ -55,18 +55,30 @@ def main():
     ap.add_argument("--nlp-steps", type=int, default=5, metavar="K",
                     help="secondary leg: K batches of the same egos solved with the drop-in default (Gauss-Newton "
                          "SQP to the reference NLP optimum, trajectory_tracking.SQP_ITERS / sqp_tol); 0: skip")
-    ap.add_argument("--closed-loop", type=int, default=0, metavar="B",
-                    help="also run B egos through the device closed loop (mpc_closed_loop, SURVEY 8(f)1) on the "
-                         "config's trajectory and FSM preset and report closed-loop ego-steps/s")
+    ap.add_argument("--closed-loop", type=int, default=512, metavar="B",
+                    help="also run B egos per GPU through the device closed loop (mpc_closed_loop, SURVEY 8(f)1) "
+                         "on the config's trajectory and FSM preset, gather their check quantities to rank 0 and "
+                         "report closed-loop ego-steps/s (0: skip)")
+    ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
+                    help="cpu: a stand-in that runs the same sharded path on libmpcqp's host backend (device = -1) "
+                         "with gloo, for the launcher tests; never a measurement")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launched as `python bench.py --gpus N`: start N rank processes before this process touches a GPU
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; run it with --gpus equal to the "
+                         "number of rank processes")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = args.device == "gpu"
 
     import numpy as np
     import torch
     import torch.distributed as dist
     import __graft_entry__ as ge
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # one build per node (a no-op when the in-tree libraries are current); the other ranks load them
     # after the barrier below
     if local == 0:
@@ -74,13 +86,16 @@ def main():
     import mpcqp
     import workloads as W
 
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU (libmpcqp has no CPU backend)")
-    torch.cuda.set_device(local)
+    if gpu:
+        if not torch.cuda.is_available():
+            raise SystemExit("bench.py needs a GPU (the measurement runs libmpcqp's HIP kernels; --device cpu is "
+                             "a test stand-in, not a measurement)")
+        torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("nccl" if gpu else "gloo", init_method="env://")
         dist.barrier()
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local) if gpu else torch.device("cpu")
+    dev_index = local if gpu else -1
 
     import shard
     cfg = W.CONFIGS[args.config]
@@ -89,42 +104,59 @@ def main():
     wb = W.make_batch(args.config, B=hi - lo, offset=lo)
     N, mo = wb["N"], wb["max_obs"]
     X, U = W.loader(wb["traj"]).X_ref, W.loader(wb["traj"]).U_ref
-    slv = mpcqp.Solver(X, U, mpcqp.default_params(N=N, max_obs=mo), device=local)
+    slv = mpcqp.Solver(X, U, mpcqp.default_params(N=N, max_obs=mo), device=dev_index)
 
-    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
-    x0 = t(wb["x0"])
-    obs = t(wb["obs"]) if wb["obs"] is not None else None
-    nob = t(wb["n_obs"], torch.int32) if wb["n_obs"] is not None else None
-    u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
-    Uo = torch.empty((B, N, 2), dtype=torch.float64, device=dev)
-    Xo = torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev)
-    st = torch.empty(B, dtype=torch.int32, device=dev)
-    it = torch.empty(B, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    ptr = lambda x: 0 if x is None else x.data_ptr()
+    if gpu:
+        t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+        x0 = t(wb["x0"])
+        obs = t(wb["obs"]) if wb["obs"] is not None else None
+        nob = t(wb["n_obs"], torch.int32) if wb["n_obs"] is not None else None
+        u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
+        Uo = torch.empty((B, N, 2), dtype=torch.float64, device=dev)
+        Xo = torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev)
+        st = torch.empty(B, dtype=torch.int32, device=dev)
+        it = torch.empty(B, dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        ptr = lambda x: 0 if x is None else x.data_ptr()
 
-    def step():
-        slv.solve_batch_device(B, ptr(x0), ptr(obs), ptr(nob), 0, ptr(u0), ptr(Uo), ptr(Xo), ptr(st), ptr(it),
-                               stream=stream.cuda_stream)
+        def step():
+            slv.solve_batch_device(B, ptr(x0), ptr(obs), ptr(nob), 0, ptr(u0), ptr(Uo), ptr(Xo), ptr(st), ptr(it),
+                                   stream=stream.cuda_stream)
+        sync = lambda: torch.cuda.synchronize(dev)
+    else:
+        host = {}
+
+        def step():
+            host.update(slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"]))
+        sync = lambda: None
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    sync()
+    if gpu:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    ev[0].record(stream)
+    tk = [t0]
+    if gpu:
+        ev[0].record(stream)
     for i in range(args.steps):
         step()
-        ev[i + 1].record(stream)
-    torch.cuda.synchronize(dev)
+        if gpu:
+            ev[i + 1].record(stream)
+        else:
+            tk.append(time.perf_counter())
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     wall = time.perf_counter() - t0
-    step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)])
+    if gpu:
+        step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)])
+    else:
+        step_ms = np.diff(np.array(tk)) * 1e3
     gpu_s = float(step_ms.sum()) / 1e3
     elapsed = max(wall, gpu_s)
     if world > 1:
@@ -133,7 +165,9 @@ def main():
         elapsed = float(tt.item())
 
     # the one collective: gather of per-rank solver telemetry (after the timed region)
-    tel = shard.reduce_telemetry(shard.gather_telemetry(shard.telemetry(st.cpu().numpy(), it.cpu().numpy()),
+    st_h = st.cpu().numpy() if gpu else host["status"]
+    it_h = it.cpu().numpy() if gpu else host["iters"]
+    tel = shard.reduce_telemetry(shard.gather_telemetry(shard.telemetry(st_h, it_h),
                                                         device=dev if world > 1 else None))
     kmean = tel["mean_iters"]
     avg_launch_s = gpu_s / args.steps
@@ -157,7 +191,7 @@ def main():
             traffic = None
 
     # closed-loop leg on every rank (its own ego shard), one gather to rank 0; after the headline timing
-    cl = closed_loop(args.config, args.closed_loop, N, local, world, rank, dev) if args.closed_loop else None
+    cl = closed_loop(args.config, args.closed_loop, N, dev_index, world, rank, dev) if args.closed_loop else None
 
     if rank == 0:
         out = {
@@ -198,20 +232,63 @@ def main():
                                  "PMC HBM bytes per step (profiles/pmc_hbm_bytes.json)",
                          "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
         }
-        if args.nlp_steps > 0:
+        if not gpu:
+            out["device"] = "cpu-standin"
+            out["note"] = ("--device cpu: libmpcqp's host backend with gloo, a stand-in for the launcher tests; "
+                           "the roofline fields are not a GPU measurement")
+        if args.nlp_steps > 0 and gpu:
             out["nlp_sqp"] = nlp_leg(args.nlp_steps, wb, B, N, mo, X, U, dev)
-        if args.inflight > 1:
+        if args.inflight > 1 and gpu:
             head = {k: v.cpu().numpy() for k, v in (("st", st), ("it", it), ("U", Uo))}
             out["inflight"] = inflight(args.inflight, args.steps, wb, B, N, mo, X, U, dev, head)
         if cl is not None:
             out["closed_loop"] = cl
-        if not args.no_cpu:
+        if not args.no_cpu and gpu:
             out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
             out["cpu_backend"] = cpu_backend(wb, N, mo, min(args.cpu_seconds, 5.0))
             out["cpu_reference"] = cpu_reference(wb, N, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` without torchrun: start N rank processes (torch.distributed.run as a child
+    process, rendezvous on 127.0.0.1) before this process makes any GPU call, pass their output through, and
+    check rank 0's JSON line.  Returns the exit code: non-zero when N exceeds the visible devices, when a rank
+    fails, or when rank 0's line does not report n_gpus == N."""
+    import socket
+    import subprocess
+    if args.device == "gpu":
+        import torch
+        visible = torch.cuda.device_count()        # counts devices without initialising HIP on this image
+        if args.gpus > visible:
+            print(f"bench.py: --gpus {args.gpus} but only {visible} GPU(s) are visible", file=sys.stderr)
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for ln in proc.stdout:
+        sys.stdout.write(ln)
+        sys.stdout.flush()
+        if ln.startswith("{"):
+            line = ln
+    rc = proc.wait()
+    if rc != 0:
+        return rc
+    if line is None:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    got = json.loads(line).get("n_gpus")
+    if got != args.gpus:
+        print(f"bench.py: rank 0 reports n_gpus={got}, expected {args.gpus}", file=sys.stderr)
+        return 1
+    return 0
 
 
 def nlp_leg(steps, wb, B, N, mo, X, U, dev):
@@ -248,7 +325,8 @@ def nlp_leg(steps, wb, B, N, mo, X, U, dev):
     slv.close()
     return {"value": B * steps / (ms.sum() / 1e3), "unit": "solves/s", "ms_per_batch": float(ms.mean()),
             "p50_batch_latency_ms": float(np.median(ms)), "sqp_iters_cap": TT.SQP_ITERS, "sqp_tol": p.sqp_tol,
-            "mean_pdip_iters": float(it.mean()), "status_counts": np.bincount(st, minlength=4).tolist(),
+            "mean_pdip_iters": float(it.mean()), "status_counts": np.bincount(st & 15, minlength=4).tolist(),
+            "sqp_unconverged": int(((st & 16) != 0).sum()),
             "note": "drop-in default of the Python surface (TrajectoryTracker.solve): SQP re-linearisations until "
                     "U moves by <= sqp_tol (or a 2-cycle / 5 elastic QPs in a row, include/mpcqp.h); secondary, the headline is the single tracking QP"}
 

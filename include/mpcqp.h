@@ -36,6 +36,10 @@ extern "C" {
 #define MPC_MAX_ITER 1        /* iteration limit hit; best iterate returned                  */
 #define MPC_INFEASIBLE 2      /* solved, but elastic slack active: hard QP(ubar) infeasible  */
 #define MPC_NUMERICAL 3       /* numerical breakdown; best iterate returned                  */
+/* flag OR-ed onto the last QP's code (status & MPC_STATUS_MASK) when sqp_iters > 1 and sqp_tol > 0 and the
+ * SQP stopped without a QP moving U by <= sqp_tol: the sqp_iters cap, a 2-cycle or the elastic-QP streak */
+#define MPC_SQP_UNCONVERGED 16
+#define MPC_STATUS_MASK 15
 
 /* return codes */
 #define MPC_SUCCESS 0

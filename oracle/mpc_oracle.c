@@ -1151,7 +1151,7 @@ int orc_solve(const orc_table* t, const mpc_params* p, const double x0[5], const
     int nsqp = p->sqp_iters < 0 ? 0 : p->sqp_iters;   /* 0: U = ubar */
     double u2[2 * MAXN];                              /* U two QPs back (for the cycle test) */
     memcpy(u2, ub, sizeof(double) * 2 * N);
-    int ninf = 0;
+    int ninf = 0, conv = 0;
     memcpy(Uo, ub, sizeof(double) * 2 * N);
     for (int it = 0; it < nsqp; ++it) {
         build_stage_qp(t, p, x0, obs, nobs, ub, &Q);
@@ -1169,7 +1169,7 @@ int orc_solve(const orc_table* t, const mpc_params* p, const double x0[5], const
         memcpy(ub, Uo, sizeof(double) * 2 * N);
         ninf = status == MPC_INFEASIBLE ? ninf + 1 : 0;
         if (nsqp > 1) {
-            if (step <= p->sqp_tol) break;                               /* converged re-linearisation */
+            if (step <= p->sqp_tol) { conv = 1; break; }                 /* converged re-linearisation */
             if (p->sqp_tol > 0.0) {                                      /* sqp_tol 0: all sqp_iters QPs */
                 if (it >= 2 && back2 <= SQP_CYCLE_REL * step) break;     /* 2-cycle: back where it was */
                 if (ninf >= SQP_INF_STREAK) break;                       /* elastic QPs in a row */
@@ -1180,6 +1180,7 @@ int orc_solve(const orc_table* t, const mpc_params* p, const double x0[5], const
     if (u0) { u0[0] = Uo[0]; u0[1] = Uo[1]; }
     if (Xpred) orc_predict(t, p, x0, Uo, Xpred);                 /* :261 */
     if (iters) *iters = total;
+    if (nsqp > 1 && p->sqp_tol > 0.0 && !conv) status |= MPC_SQP_UNCONVERGED;
     return status;
 }
 

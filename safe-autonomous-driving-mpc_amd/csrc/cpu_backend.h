@@ -154,6 +154,7 @@ public:
         std::memcpy(u2, ub, sizeof(double) * 2 * N);
         const int nsqp = p_.sqp_iters < 0 ? 0 : p_.sqp_iters;
         int status = MPC_OK, total = 0, ninf = 0;
+        bool conv = false;
         for (int it = 0; it < nsqp; ++it) {
             build(x0, obs, nobs, ub);
             int ni = 0;
@@ -169,7 +170,7 @@ public:
             std::memcpy(ub, uo, sizeof(double) * 2 * N);
             ninf = status == MPC_INFEASIBLE ? ninf + 1 : 0;
             if (nsqp > 1) {
-                if (step <= p_.sqp_tol) break;                                   // re-linearisation converged
+                if (step <= p_.sqp_tol) { conv = true; break; }                  // re-linearisation converged
                 if (p_.sqp_tol > 0.0 && ((it >= 2 && back2 <= kCycleRel * step) || ninf >= kInfStreak)) break;
             }
         }
@@ -177,6 +178,7 @@ public:
         if (u0) { u0[0] = uo[0]; u0[1] = uo[1]; }
         if (Xpred) predict(x0, uo, reinterpret_cast<double(*)[5]>(Xpred));    // :261
         if (iters) *iters = total;
+        if (nsqp > 1 && p_.sqp_tol > 0.0 && !conv) status |= MPC_SQP_UNCONVERGED;
         return status;
     }
 

@@ -1172,6 +1172,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     // left (2 bits per row, then one per box row), which starts the next QP's crossover (oracle polish_from,
     // given = 2); U two QPs back at this lane's control; the count of elastic QPs in a row
     int wcls = 0, ninf = 0;
+    bool sqp_conv = false;
     double pb0 = 0.0, pb1 = 0.0;
     bool xo_ok = false;                    // MODE_XO: the crossover certified this instance
     double cstr[6] = {0, 0, 0, 0, 0, 0};   // LITE: cost data of stage k (this lane's only)
@@ -1885,10 +1886,12 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             pb0 = ua0;
             pb1 = ua1;
             ninf = status == MPC_INFEASIBLE ? ninf + 1 : 0;
-            if (stp <= Pr.sqp_tol) break;
+            if (stp <= Pr.sqp_tol) { sqp_conv = true; break; }
             if (Pr.sqp_tol > 0.0 && ((sqp >= 2 && b2 <= SQP_CYCLE_REL * stp) || ninf >= SQP_INF_STREAK)) break;
         }
     }
+
+    if (MODE == MODE_FULL && nsqp > 1 && Pr.sqp_tol > 0.0 && !sqp_conv) status |= MPC_SQP_UNCONVERGED;
 
     // ---- K5: outputs: U*, u0, predict(x0, U*) ----------------------------------------------
     PROF(9)

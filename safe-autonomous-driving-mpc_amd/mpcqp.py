@@ -14,6 +14,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmpcqp.so")
 
 MPC_OK, MPC_MAX_ITER, MPC_INFEASIBLE, MPC_NUMERICAL = 0, 1, 2, 3
+# flag OR-ed onto the last QP's status when the SQP (sqp_iters > 1, sqp_tol > 0) stopped unconverged
+MPC_SQP_UNCONVERGED, MPC_STATUS_MASK = 16, 15
 STATUS_NAMES = {0: "ok", 1: "max_iter", 2: "infeasible", 3: "numerical"}
 MAX_N = 63
 MAX_OBS = 64

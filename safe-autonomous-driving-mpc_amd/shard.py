@@ -7,7 +7,8 @@ collective is the final gather of per-rank solver telemetry to rank 0 (RCCL over
 """
 import numpy as np
 
-TELEMETRY_FIELDS = ("ok", "max_iter", "infeasible", "numerical", "iters_sum", "iters_max", "n")
+TELEMETRY_FIELDS = ("ok", "max_iter", "infeasible", "numerical", "iters_sum", "iters_max", "n", "sqp_unconverged")
+SQP_UNCONVERGED, STATUS_MASK = 16, 15     # include/mpcqp.h
 
 
 def shard_range(total, world, rank):
@@ -23,8 +24,9 @@ def telemetry(status, iters):
     """Per-rank summary vector (float64) of one batched solve: status counts, iteration sum/max, size."""
     status = np.asarray(status).ravel()
     iters = np.asarray(iters).ravel()
-    counts = [float((status == k).sum()) for k in range(4)]
-    return np.array(counts + [float(iters.sum()), float(iters.max(initial=0)), float(status.size)], np.float64)
+    counts = [float(((status & STATUS_MASK) == k).sum()) for k in range(4)]
+    return np.array(counts + [float(iters.sum()), float(iters.max(initial=0)), float(status.size),
+                              float(((status & SQP_UNCONVERGED) != 0).sum())], np.float64)
 
 
 def gather_telemetry(vec, device=None):
@@ -47,7 +49,7 @@ def reduce_telemetry(mat):
     n = mat[:, 6].sum()
     return {"status_counts": {k: int(mat[:, i].sum()) for i, k in enumerate(TELEMETRY_FIELDS[:4])},
             "mean_iters": float(mat[:, 4].sum() / max(n, 1.0)), "max_iters": int(mat[:, 5].max()),
-            "egos": int(n), "ranks": int(mat.shape[0])}
+            "egos": int(n), "ranks": int(mat.shape[0]), "sqp_unconverged": int(mat[:, 7].sum())}
 
 
 # ---------------------------------------------------------------------------------------------

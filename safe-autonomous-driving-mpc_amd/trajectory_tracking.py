@@ -304,26 +304,35 @@ def run_simulation_batch(mpc, fsm, trajectory, x_init=None, B=1, max_steps=2000,
     x_init = np.asarray(x_init, np.float64).reshape(-1, 5)
     r = mpc.solver(max_obs=0).closed_loop(x_init, fsm_params(fsm), max_steps=max_steps, s_max=trajectory.s_max)
     if checks:
-        import contextlib
-        import io
-        ok = np.zeros(x_init.shape[0], bool)
-        for b in range(x_init.shape[0]):
-            n = int(r["n_steps"][b])
-            step_s = np.full(n, np.nanmedian(r["step_ms"][:n]) / 1e3 / x_init.shape[0]) if n else np.zeros(0)
-            f = ObstaclesFSM(fsm.dynamic_obstacle, fsm.traffic_light) if fsm is not None else ObstaclesFSM()
-            if fsm is not None:
-                for k in FSM_PRESETS["trajectory2"]:
-                    setattr(f, k, getattr(fsm, k))
-            buf = io.StringIO()
-            tl = ["GREEN" if t == 1 else "RED" for t in r["hist_tl"][b, :n]]
-            with contextlib.redirect_stdout(buf):
-                ok[b] = bool(trajectory_tracking_check(mpc, list(r["hist_x"][b, :n + 1]), list(r["hist_u"][b, :n]),
-                                                       list(step_s), list(r["hist_obs_s"][b, :n]), tl, f,
-                                                       trajectory.s_max))
-            if verbose:
-                print(buf.getvalue())
-        r["checks_passed"] = ok
+        r["checks_passed"] = closed_loop_checks(mpc, fsm, trajectory, r, verbose)
     return r
+
+
+def closed_loop_checks(mpc, fsm, trajectory, r, verbose=False):
+    """The restated trajectory_tracking_check (sanity_checks.py:79-184) on every ego of a closed_loop()
+    result (mpcqp.Solver.closed_loop layout); returns the per-ego verdicts [B] (bool)."""
+    import contextlib
+    import io
+    B = np.asarray(r["n_steps"]).size
+    ok = np.zeros(B, bool)
+    for b in range(B):
+        n = int(r["n_steps"][b])
+        # the solve time this ego waited for at each of its steps: that batched step's device time
+        # (the reference tests max(hist_t) per step, sanity_checks.py:134-135; shard.closed_loop_quantities)
+        step_s = np.asarray(r["step_ms"][:n], np.float64) / 1e3
+        f = ObstaclesFSM(fsm.dynamic_obstacle, fsm.traffic_light) if fsm is not None else ObstaclesFSM()
+        if fsm is not None:
+            for k in FSM_PRESETS["trajectory2"]:
+                setattr(f, k, getattr(fsm, k))
+        buf = io.StringIO()
+        tl = ["GREEN" if t == 1 else "RED" for t in r["hist_tl"][b, :n]]
+        with contextlib.redirect_stdout(buf):
+            ok[b] = bool(trajectory_tracking_check(mpc, list(r["hist_x"][b, :n + 1]), list(r["hist_u"][b, :n]),
+                                                   list(step_s), list(r["hist_obs_s"][b, :n]), tl, f,
+                                                   trajectory.s_max))
+        if verbose:
+            print(buf.getvalue())
+    return ok
 
 
 if __name__ == "__main__":

@@ -163,3 +163,32 @@ def test_traj2_fsm_closed_loop_vs_reference_run(env):
     ho = r["hist_obs_s"][0, :n]
     assert np.array_equal(np.isnan(ho), np.isnan(obs_s)) and np.array_equal(ho[~np.isnan(ho)], obs_s[~np.isnan(obs_s)])
     assert np.array_equal(r["hist_tl"][0, :n], np.array(tl))
+
+
+def test_sqp_unconverged_flag(env):
+    """MPC_SQP_UNCONVERGED (16) marks the SQP runs that stopped without a QP moving U by <= sqp_tol (the
+    sqp_iters cap, a 2-cycle or the elastic streak; status & 15 keeps the last QP's code).  On C2 egos with
+    the drop-in default: the backend and the oracle flag the same egos, some egos are flagged, and a flagged
+    ego's U is not a fixed point of the SQP while an unflagged ego's is (one more QP from U)."""
+    mpcqp, O, TT, W, _, _ = env
+    w = W.make_batch("C2")
+    x0 = w["x0"][:1024]
+    ld = W.loader(w["traj"])
+    p = mpcqp.default_params(N=20, sqp_iters=TT.SQP_ITERS)
+    r = mpcqp.Solver(ld.X_ref, ld.U_ref, p, device=-1).solve_batch(x0)
+    ro = O.Oracle(ld.X_ref, ld.U_ref).solve_batch(O.default_params(N=20, sqp_iters=TT.SQP_ITERS), x0)
+    assert np.array_equal(r["status"], ro["status"])
+    flag = (r["status"] & mpcqp.MPC_SQP_UNCONVERGED) != 0
+    assert flag.sum() > 0 and set(np.unique(r["status"] & mpcqp.MPC_STATUS_MASK)) <= {0, 2}
+    one = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=20, sqp_iters=1), device=-1)
+    sel = np.concatenate([np.flatnonzero(flag), np.flatnonzero(~flag)[:64]])
+    again = one.solve_batch(x0[sel], ubar=r["U"][sel])
+    move = np.abs(again["U"] - r["U"][sel]).reshape(len(sel), -1).max(axis=1)
+    nf = int(flag.sum())
+    print(f"flagged {nf} of {len(x0)}; one more QP moves flagged U by >= {move[:nf].min():.1e}, "
+          f"unflagged by <= {move[nf:].max():.1e}")
+    # unflagged egos are fixed points; every flagged one moves by more than any unflagged one (most of them by
+    # far more: 2-cycles and elastic wandering; the rest stopped on the cap or the cycle rule just short of
+    # sqp_tol, which the flag reports conservatively)
+    assert (move[nf:] <= 1e-8).all() and move[:nf].min() > move[nf:].max()
+    assert (move[:nf] > 1e-8).mean() >= 0.75

@@ -159,7 +159,11 @@ def check_vs_oracle(r, ro, ctx=None, label="", tol=TOL_U, xtol=1e-8):
     its elastic optimum (status 2, KKT-checked by the polish) must have an objective no worse than the
     other's.  U must agree to TOL_U wherever both sides certified a solution, except on elastic instances
     (status 2 on both) whose two answers have the same elastic objective to 1e-9 relative: the polish can
-    certify two points of one flat elastic optimum ("Elastic-problem tolerance")."""
+    certify two points of one flat elastic optimum ("Elastic-problem tolerance").
+    The SQP-unconverged flag (16) is compared separately: it must agree wherever U agrees."""
+    flag_g, flag_o = (r["status"] & 16) != 0, (ro["status"] & 16) != 0
+    r = dict(r, status=r["status"] & 15)
+    ro = dict(ro, status=ro["status"] & 15)
     agree = r["status"] == ro["status"]
     mism = ~agree
     assert np.isin(r["status"][mism], (2, 3)).all() and np.isin(ro["status"][mism], (2, 3)).all(), \
@@ -185,7 +189,9 @@ def check_vs_oracle(r, ro, ctx=None, label="", tol=TOL_U, xtol=1e-8):
     ok = cert & (err <= tol)
     xe = np.abs(r["Xpred"] - ro["Xpred"]).reshape(len(cert), -1).max(axis=1)
     assert xe[ok].max(initial=0.0) <= xtol, (label, xe[ok].max())
+    assert np.array_equal(flag_g[ok], flag_o[ok]), (label, np.flatnonzero(ok & (flag_g != flag_o)))
     s = dict(label=label, B=len(cert), status_agree=float(agree.mean()), flips_2_3=int(mism.sum()),
+             sqp_unconverged=int(flag_g.sum()),
              elastic_alt_optima=alt, max_err_U=float(err[ok].max(initial=0.0)),
              max_err_Xpred=float(xe[ok].max(initial=0.0)))
     print(json.dumps(s))

@@ -165,3 +165,28 @@ def test_two_rank_closed_loop_gather_matches_single_process(tmp_path):
     assert int(rep["passed"]) == passed
     # the scenarios ran: the light switched for the egos starting before it, the car appeared for the others
     assert (r["hist_tl"][0::2] == 1).any(axis=1).all() and np.isfinite(r["hist_obs_s"][1::2]).any(axis=1).all()
+
+
+def test_realtime_check_sees_the_slowest_step(capsys):
+    """Both restatements of the real-time check (sanity_checks.py:133-139, max(hist_t) per step) must fail an
+    ego whose run contains one 151 ms step, and pass an ego that left the loop before that step:
+    trajectory_tracking.closed_loop_checks (run_simulation_batch) and shard.closed_loop_quantities +
+    check_verdicts (the bench's gathered path)."""
+    import shard
+    import trajectory_tracking as TT
+    from sanity_checks import check_verdicts
+    r, traj = cpu_closed_loop(cl_inputs(2), 12)
+    r["n_steps"] = np.array([12, 3], np.int32)      # ego 1 left the loop after 3 steps
+    r["step_ms"] = np.ones(12)
+    r["step_ms"][5] = 151.0                         # a step only ego 0 executed
+    fsm = TT.ObstaclesFSM(True, True)
+    capsys.readouterr()
+    TT.closed_loop_checks(TT.TrajectoryTracker(traj), fsm, traj, r, verbose=True)
+    blocks = capsys.readouterr().out.split("=== SANITY CHECKS ===")[1:]
+    assert len(blocks) == 2
+    assert "Real-time constraint respected : False --> Max CPU time 151.0ms > 150ms" in blocks[0]
+    assert "Real-time constraint respected : True" in blocks[1]
+    q = shard.closed_loop_quantities(r, 0, True, True, fsm.tl_pos)
+    v = [check_verdicts(dict(zip(shard.CL_FIELDS, row)), (-0.6, -5.0), (0.6, 4.0), traj.s_max) for row in q]
+    assert not v[0]["realtime"] and v[1]["realtime"]
+    assert q[0, shard.CL_FIELDS.index("max_cpu_ms")] == 151.0
