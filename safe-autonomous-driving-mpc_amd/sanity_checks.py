@@ -4,6 +4,10 @@ Same checks, tolerances and prints as sanity_checks.py:79-184 of the reference
 (destination within 1 m, |d| <= 1.5 m, controls within bounds +-0.1, max solve time <= 150 ms,
 dynamic-obstacle gap >= 1 m, no RED-light pass).  Returns the bool like the reference.
 `check_summary` is the silent, structured form used by the batched closed loop and the bench.
+
+reference_trajectory_check restates the planner's acceptance check (sanity_checks.py:3-75), including its
+AND at :48 and :54 (a control check fails only when both of its limits are exceeded); `plan_check_summary`
+is its silent form.
 """
 import numpy as np
 
@@ -92,3 +96,55 @@ def trajectory_tracking_check(tracker, hist_x, hist_u, hist_t, hist_obs_s, hist_
               else 'Traffic Light Respected : True')
     print(f'===> Checks passed : {r["passed"]}')
     return r["passed"]
+
+
+# ---------------------------------------------------------------------------------------------
+# offline planner acceptance check (sanity_checks.py:3-75)
+# ---------------------------------------------------------------------------------------------
+PLAN_DISTANCE_TOL = 0.5      # m
+PLAN_VELOCITY_TOL = 0.1
+PLAN_CONTROLS_TOL = 0.1
+PLAN_LATERAL_DEV_TOL = 1.5   # m
+PLAN_SLACK_TOL = 0.1
+
+
+def plan_check_summary(u_min, u_max, X, U, S, s_total):
+    """The measurements and verdicts of reference_trajectory_check, without printing."""
+    X, U, S = np.asarray(X, np.float64), np.asarray(U, np.float64).reshape(-1, 2), np.asarray(S, np.float64)
+    q = {"error_s": abs(X[-1, 0] - s_total), "v_final": X[-1, 4], "min_v": np.min(X[:, 4]),
+         "max_lat_dev": np.max(np.abs(X[:, 1])), "max_slack": np.max(np.abs(S))}
+    q["destination"] = not (q["error_s"] > PLAN_DISTANCE_TOL)                                 # :19-25
+    q["full_stop"] = not (abs(q["v_final"]) > PLAN_VELOCITY_TOL)                             # :27-33
+    q["forward"] = not (q["min_v"] < -PLAN_VELOCITY_TOL)                                     # :35-41
+    # :48 and :54: a control check fails only if BOTH of its limits are exceeded (the reference's AND)
+    q["u1_ok"] = not (np.min(U[:, 0]) < u_min[0] - PLAN_CONTROLS_TOL and np.max(U[:, 0]) > u_max[0] + PLAN_CONTROLS_TOL)
+    q["u2_ok"] = not (np.min(U[:, 1]) < u_min[1] - PLAN_CONTROLS_TOL and np.max(U[:, 1]) > u_max[1] + PLAN_CONTROLS_TOL)
+    q["lateral_ok"] = not (q["max_lat_dev"] > PLAN_LATERAL_DEV_TOL)                          # :59-65
+    q["slack_ok"] = not (q["max_slack"] > PLAN_SLACK_TOL)                                    # :67-73
+    passed = q["destination"] and q["full_stop"] and q["forward"]
+    if passed:                                                                               # :50-51, :56-57
+        passed = q["u1_ok"]
+    if passed:
+        passed = q["u2_ok"]
+    q["passed"] = bool(passed and q["lateral_ok"] and q["slack_ok"])
+    return q
+
+
+def reference_trajectory_check(optimizer, X, U, S, s_total):
+    """Verifies the physical feasibility of a planned reference trajectory (prints like the reference,
+    sanity_checks.py:3-75; returns None like it, see plan_check_summary for the verdicts)."""
+    print("\n=== SANITY CHECKS ===")
+    q = plan_check_summary(optimizer.u_min, optimizer.u_max, X, U, S, s_total)
+    print(f'Final destination reached : False --> Error = {q["error_s"]} m' if not q["destination"]
+          else 'Final destination reached : True')
+    print(f'Full stop at the end : False --> Final velocity = {q["v_final"] * 3.6} km/h' if not q["full_stop"]
+          else 'Full stop at the end : True')
+    print(f'Always non-negative velocity : False --> Minimum velocity = {q["min_v"] * 3.6} km/h' if not q["forward"]
+          else 'Always non-negative velocity : True')
+    print(f'Curvature rate limits respected : {q["u1_ok"]}')
+    print(f'Acceleration limits respected : {q["u2_ok"]}')
+    print(f'Lateral deviation respected : False --> Maximum lateral deviation : {q["max_lat_dev"]} m'
+          if not q["lateral_ok"] else 'Lateral deviation respected : True')
+    print(f'Low slack usage : False --> Maximum slack value : {q["max_slack"]}' if not q["slack_ok"]
+          else 'Low slack usage : True')
+    print(f'===> Checks passed : {q["passed"]}')
