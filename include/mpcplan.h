@@ -1,0 +1,112 @@
+/* mpcplan.h — C ABI of the MI355X batched offline planner (libmpcplan.so).
+ *
+ * Replaces the chunk solve of the reference's offline planner:
+ *   TrajectoryOptimizer.optimize(x0, s_target, s_total, k_ref_fun, v_min_fun, v_max_fun, is_final_chunk)
+ *   (/root/reference/trajectory_planning.py:351-390): a Hermite-Simpson collocation NLP over
+ *   z = [X (N+1)x5, U Nx2, S N] (:91-126) with the cost of :128-170 and the constraints of :172-349, solved
+ *   by scipy SLSQP (maxiter 500, ftol 1e-4, :381-387).
+ * and the route functions it is called with (optimize_full_trajectory, :437-477): k_ref_fun (curvature of
+ * the route's parametric CubicSpline at t = s_to_t(s), :439-459) and v_max_fun (interp1d kind='previous'
+ * over the route's speed-limit array, :463-473); v_min_fun = 0 (:476-477).
+ *
+ * Here B independent chunks (any mix of routes' positions, intermediate or final) are solved in one call:
+ * a Gauss-Newton SQP on the same NLP, each QP by a Mehrotra primal-dual interior point on the stage-wise
+ * Riccati recursion, FP64, one chunk per GPU lane ("Offline planner").
+ *
+ * Reference quirks restated:
+ *   - the defect rule.  The committed source computes x_pred = x_k - dt/6 (f_k + 4 f_mid + f_{k+1})
+ *     (:205); the committed planner outputs (trajectories/*.json, committed data) satisfy x_{k+1} = x_k + dt/6 (...)
+ *     instead (v_{k+1} - v_k = +dt u2_k to 1e-10 on all three).  defect_sign = +1 (default) is the rule the
+ *     outputs obey, -1 the source's literal sign;
+ *   - the intermediate-chunk terminal row is s_N >= s_target / 2 (:238-246), half of the ABSOLUTE target;
+ *   - the slack only relaxes the speed bounds' lower side in effect (v + S >= v_min, v + S <= v_max, S >= 0);
+ *     the last state has no slack (:253-256);
+ *   - v_max(s) below the first route knot is NaN in the reference (interp1d 'previous' extrapolation); here
+ *     it is the first knot's limit.
+ * The final chunk's terminal equalities (s_N = s_target, v_N = 0, :221-236) are solved exactly; there the
+ * speed and lateral-acceleration rows of x_N, which v_N = 0 satisfies, are left out.  The rows of x_0 alone
+ * (curvature, lateral acceleration) are constants fixed by x0 and are left out (x_0 = x0 is exact).
+ */
+#ifndef MPCPLAN_H
+#define MPCPLAN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCPLAN_VERSION 1
+#define PLAN_MAX_N 64          /* collocation intervals per chunk */
+
+/* status[] codes */
+#define PLAN_OK 0              /* SQP converged (a QP moved z by <= sqp_tol)                          */
+#define PLAN_NOT_CONVERGED 1   /* sqp_iters QPs ran (or a 2-cycle) without convergence; last iterate   */
+#define PLAN_QP_FAILED 2       /* a QP's interior point did not converge (infeasible linearisation)   */
+#define PLAN_NUMERICAL 3       /* non-finite values; last finite iterate                               */
+#define PLAN_FROZEN_LIMITS 4   /* converged after freezing the speed limits at a band change (a 2-cycle:
+                                  the reference NLP has no optimum there), feasible for the reference rows */
+
+/* return codes */
+#define PLAN_SUCCESS 0
+#define PLAN_E_ARG (-1)
+#define PLAN_E_DEVICE (-2)
+#define PLAN_E_ALLOC (-3)
+#define PLAN_E_LAUNCH (-4)
+
+/* TrajectoryOptimizer.__init__ (trajectory_planning.py:14-47) plus solver knobs. */
+typedef struct {
+    int N;                 /* intervals, when plan_solve_chunks gets no per-chunk N (reference: :515)   */
+    double dt;             /* 0.3 s (:514)                                                             */
+    double w_y, w_s, w_u, w_slack;   /* 10, 10, 0.1, 100 (:14)                                         */
+    double u_min[2], u_max[2];       /* (-0.6, -5), (0.6, 4) (:35-36)                                  */
+    double k_min, k_max;             /* -0.8, 0.8 (:43-44)                                             */
+    double a_max;                    /* 6 (:47)                                                        */
+    double v_min;                    /* 0 (v_min_fun, :476-477)                                        */
+    double defect_sign;              /* +1 (see the header comment)                                    */
+    int sqp_iters;                   /* cap on QPs per chunk (reference: SLSQP maxiter 500)             */
+    double sqp_tol;                  /* converged when a QP moves z by <= sqp_tol (max norm)            */
+    int max_iter;                    /* interior-point iterations per QP                                */
+    double tol;                      /* interior-point tolerance (complementarity, row residuals)       */
+} plan_params;
+
+typedef struct plan_ctx plan_ctx;
+
+void plan_default_params(plan_params* p);
+
+/* The route (optimize_full_trajectory's reference path, :435-477), copied into the context:
+ *   s[M]        cumulative chord length of the detailed way-points (unpack_reference_path, :411-414),
+ *               strictly increasing; s_total = s[M-1];
+ *   cx, cy      [M-1][4] coefficients of the parametric CubicSpline x(t), y(t) over t = 0..M-1
+ *               (path_planning.create_spline), scipy PPoly order: row i holds c[0..3, i], the cubic first;
+ *   vmax[M]     speed limit at each way-point in m/s (:464-467).
+ * device >= 0: HIP device index; there is no host backend (the CPU restatement is test infrastructure). */
+int plan_create(const double* s, int M, const double* cx, const double* cy, const double* vmax,
+                const plan_params* p, int device, plan_ctx** out);
+
+/* B chunks, host buffers, synchronous.  Per chunk b: x0[b][5] (current_x0, :486/:548), s_target[b]
+ * (:503), is_final[b] (:494-499), N[b] (NULL: params N; each <= PLAN_MAX_N).  s_total is the route's.
+ * Outputs with row stride Nmax = max over b of N[b]: X[b][Nmax+1][5], U[b][Nmax][2], S[b][Nmax] (rows past
+ * a chunk's own N are zero), status[b], iters[b] (interior-point iterations, all QPs), sqp[b] (QPs run);
+ * any output pointer may be NULL.  Never fails because a chunk did not converge (status[]). */
+int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const double* s_target,
+                      const int* is_final, double* X, double* U, double* S, int* status, int* iters,
+                      int* sqp);
+
+/* Same with device pointers, asynchronous on `stream` (hipStream_t; NULL = the null stream).  Nmax must
+ * bound every N[b] (N NULL: params N).  Scratch is owned by the context (grown on demand, never while a
+ * graph capture is active on the stream: then a call that needs more scratch fails with PLAN_E_ALLOC). */
+int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const double* x0,
+                             const double* s_target, const int* is_final, double* X, double* U, double* S,
+                             int* status, int* iters, int* sqp, void* stream);
+
+/* Route functions on the device, for tests: kappa(s) and dkappa/ds (k_ref_fun, :445-459), v_max(s). */
+int plan_route_eval(plan_ctx* c, int n, const double* s, double* kappa, double* dkappa, double* vmax);
+
+int plan_set_params(plan_ctx* c, const plan_params* p);
+const char* plan_last_error(void);   /* thread-local */
+int plan_version(void);
+void plan_destroy(plan_ctx* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,175 @@
+"""Routes for the offline planner: the reference path that optimize_full_trajectory builds
+(trajectory_planning.py:393-477) as the plain arrays libmpcplan takes (include/mpcplan.h, plan_create).
+
+The reference gets its route from the GraphHopper HTTP API and projects it with pymap3d
+(path_planning.py:19-107); both are network/third-party steps outside this build's scope.  Everything after
+the projection is restated here from the source:
+  - densification of the way-points to <= 5 m (add_extra_points, get_reference_path: path_planning.py:123-143,
+    :182-195);
+  - the parametric CubicSpline x(t), y(t) over t = 0..M-1 (create_spline, :146-162; scipy's CubicSpline, the
+    same library and default not-a-knot end conditions, so the coefficients are the reference's);
+  - s_values, the cumulative chord length (unpack_reference_path, trajectory_planning.py:411-414);
+  - the speed-limit array over the detailed points (get_speed_limits, path_planning.py:203-243, 30 km/h for
+    missing values; trajectory_planning.py:464-467).
+Inputs without the network: `from_waypoints` (local x, y way-points + GraphHopper-style max_speed intervals),
+`from_trajectory` (the global line of a committed trajectory, the way trajectory_loader.py:32-62 rebuilds it)
+and `synthetic` (a documented generator: curvature profile + speed-limit bands).
+"""
+import math
+
+import numpy as np
+from scipy.interpolate import CubicSpline, interp1d
+
+
+def add_extra_points(p1, p2, threshold=5.0):
+    """path_planning.add_extra_points (:123-143): recursive midpoints while the gap exceeds 5 m."""
+    if threshold < math.dist(p1, p2):
+        mid = ((p1[0] + p2[0]) / 2, (p1[1] + p2[1]) / 2)
+        return add_extra_points(p1, mid, threshold) + [mid] + add_extra_points(mid, p2, threshold)
+    return []
+
+
+def densify(points):
+    """get_reference_path (path_planning.py:182-195): original points with the extra points between them."""
+    out = []
+    for i in range(len(points) - 1):
+        out.append(tuple(points[i]))
+        out += add_extra_points(tuple(points[i]), tuple(points[i + 1]))
+    out.append(tuple(points[-1]))
+    return out
+
+
+class Route:
+    """A planner route: detailed way-points (M, 2) in local metres and the speed limit at each (m/s)."""
+
+    def __init__(self, detailed_points, v_max_points, name="route"):
+        pts = np.asarray(detailed_points, np.float64)
+        if pts.ndim != 2 or pts.shape[1] != 2 or pts.shape[0] < 3:
+            raise ValueError("need at least 3 detailed way-points (M, 2)")
+        self.name = name
+        self.points = pts
+        t = np.arange(len(pts))
+        self.spline = (CubicSpline(t, pts[:, 0]), CubicSpline(t, pts[:, 1]))        # create_spline
+        dist = np.sqrt(np.diff(pts[:, 0]) ** 2 + np.diff(pts[:, 1]) ** 2)              # :412
+        self.s = np.concatenate([[0], np.cumsum(dist)])                                # :413
+        if not (np.diff(self.s) > 0).all():
+            raise ValueError("consecutive way-points must be distinct")
+        self.s_total = float(self.s[-1])                                               # :414
+        self.cx = np.ascontiguousarray(self.spline[0].c.T)                            # [M-1][4], cubic first
+        self.cy = np.ascontiguousarray(self.spline[1].c.T)
+        self.vmax = np.ascontiguousarray(v_max_points, np.float64)
+        if self.vmax.shape != (len(pts),):
+            raise ValueError("one speed limit per detailed way-point")
+        # the reference's own route functions (trajectory_planning.py:440-473), for checks and the drop-in
+        self._s_to_t = interp1d(self.s, np.linspace(0.0, len(pts) - 1, len(pts)), kind="linear",
+                                fill_value="extrapolate")
+        self._vint = interp1d(self.s, self.vmax, kind="previous", fill_value="extrapolate")
+
+    @property
+    def M(self):
+        return len(self.s)
+
+    def k_ref_fun(self, s):
+        """trajectory_planning.py:445-459 (scipy evaluation, as the reference)."""
+        t = float(self._s_to_t(s))
+        xs, ys = self.spline
+        x_dt, y_dt, x_ddt, y_ddt = xs(t, 1), ys(t, 1), xs(t, 2), ys(t, 2)
+        denom = (x_dt ** 2 + y_dt ** 2) ** 1.5 + 1e-9
+        if denom < 1e-8:
+            denom = 1e-8
+        return float((x_dt * y_ddt - y_dt * x_ddt) / denom)
+
+    def v_max_fun(self, s):
+        """trajectory_planning.py:470-473 (NaN below the first knot, as interp1d 'previous' gives)."""
+        return float(self._vint(s))
+
+    def avg_speed_from(self, current_s):
+        """np.mean(v_max_array[int(current_s / 5):]) of optimize_full_trajectory (:507)."""
+        return float(np.mean(self.vmax[int(current_s / 5):]))
+
+
+def speed_limit_array(original_points, detailed_points, max_speed):
+    """get_speed_limits (path_planning.py:203-243) + trajectory_planning.py:464-467: the limit (m/s) at every
+    detailed point; max_speed = [(start_idx, end_idx, km/h or None)] over the ORIGINAL points."""
+    det = [tuple(p) for p in detailed_points]
+    v = np.ones(len(det))
+    for start, end, kmh in max_speed:
+        kmh = 30.0 if kmh is None else kmh
+        i0 = det.index(tuple(original_points[start]))
+        i1 = det.index(tuple(original_points[end]))
+        v[i0:i1 + 1] = kmh / 3.6
+    return v
+
+
+def from_waypoints(points, max_speed, name="route"):
+    """A route from local way-points (the output of path_planning.global2local) and GraphHopper-style
+    max_speed intervals over them."""
+    pts = [tuple(map(float, p)) for p in points]
+    det = densify(pts)
+    return Route(det, speed_limit_array(pts, det, max_speed), name)
+
+
+def global_line(X):
+    """The global (x, y) line of a committed trajectory, integrated like trajectory_loader.py:32-62."""
+    s = X[:, 0].copy()
+    for i in range(1, len(s)):                          # monotone fix, trajectory_loader.py:26-30
+        if s[i] <= s[i - 1]:
+            s[i] = s[i - 1] + 1e-5
+    x, y, psi = [0.0], [0.0], [0.0]
+    for i in range(1, len(s)):
+        ds = s[i] - s[i - 1]
+        pn = psi[-1] + X[i - 1, 3] * ds
+        pa = (psi[-1] + pn) / 2.0
+        x.append(x[-1] + np.cos(pa) * ds)
+        y.append(y[-1] + np.sin(pa) * ds)
+        psi.append(pn)
+    return np.column_stack([x, y])
+
+
+def from_trajectory(X, bands=((0.0, 50.0),), min_gap=1.0, name="route"):
+    """Synthetic input of realistic geometry: the global line of a committed planner output as way-points
+    (points closer than min_gap dropped), densified to <= 5 m, with speed-limit bands: (fraction of the
+    way-points where the band starts, km/h)."""
+    g = global_line(np.asarray(X, np.float64))
+    keep = [0]
+    for i in range(1, len(g)):
+        if np.hypot(*(g[i] - g[keep[-1]])) >= min_gap:
+            keep.append(i)
+    pts = [tuple(map(float, g[i])) for i in keep]
+    n = len(pts)
+    iv = []
+    for b, (frac, kmh) in enumerate(bands):
+        start = int(frac * (n - 1))
+        end = int(bands[b + 1][0] * (n - 1)) if b + 1 < len(bands) else n - 1
+        iv.append((start, end, kmh))
+    return from_waypoints(pts, iv, name)
+
+
+def synthetic(length=1500.0, seed=0, spacing=12.0, name=None):
+    """Documented synthetic route: way-points every `spacing` m along a heading that follows a random
+    piecewise-constant curvature profile (straights, and arcs of radius 15-200 m, turns up to 90 degrees),
+    with speed-limit bands of 30 / 40 / 50 km/h changing every 150-500 m (numpy default_rng(seed))."""
+    rng = np.random.default_rng(seed)
+    pts, psi, s = [(0.0, 0.0)], 0.0, 0.0
+    seg_k, seg_left = 0.0, 0.0
+    while s < length:
+        if seg_left <= 0.0:
+            if rng.uniform() < 0.45:
+                seg_k, seg_left = 0.0, rng.uniform(40.0, 200.0)
+            else:
+                radius = rng.uniform(15.0, 200.0)
+                turn = rng.uniform(0.2, np.pi / 2)
+                seg_k, seg_left = rng.choice([-1.0, 1.0]) / radius, turn * radius
+        step = min(spacing, seg_left) if seg_left > 1.0 else spacing
+        psi_new = psi + seg_k * step
+        pa = 0.5 * (psi + psi_new)
+        x, y = pts[-1]
+        pts.append((x + np.cos(pa) * step, y + np.sin(pa) * step))
+        psi, s, seg_left = psi_new, s + step, seg_left - step
+    n = len(pts)
+    iv, i = [], 0
+    while i < n - 1:
+        j = min(n - 1, i + int(rng.uniform(150.0, 500.0) / spacing))
+        iv.append((i, j, float(rng.choice([30.0, 40.0, 50.0]))))
+        i = j
+    return from_waypoints(pts, iv, name or f"synthetic{seed}")
