@@ -15,7 +15,7 @@
  *
  * Reference quirks restated:
  *   - the defect rule.  The committed source computes x_pred = x_k - dt/6 (f_k + 4 f_mid + f_{k+1})
- *     (:205); the committed planner outputs (trajectories/*.json, committed data) satisfy x_{k+1} = x_k + dt/6 (...)
+ *     (:205); the committed planner outputs (the trajectories JSON files) satisfy x_{k+1} = x_k + dt/6 (...)
  *     instead (v_{k+1} - v_k = +dt u2_k to 1e-10 on all three).  defect_sign = +1 (default) is the rule the
  *     outputs obey, -1 the source's literal sign;
  *   - the intermediate-chunk terminal row is s_N >= s_target / 2 (:238-246), half of the ABSOLUTE target;

@@ -1,0 +1,170 @@
+"""Drop-in surface of the reference's offline planner (trajectory_planning.py) on libmpcplan (MI355X).
+
+`TrajectoryOptimizer` keeps the reference's constructor, attributes, `dynamics`, `unpack` / `pack`, `cost`
+and `optimize(x0, s_target, s_total, k_ref_fun, v_min_fun, v_max_fun, is_final_chunk)` signature
+(trajectory_planning.py:8-391).  The NLP is solved on the GPU (include/mpcplan.h), so the route functions
+must be the ones of a routes.Route (its bound k_ref_fun / v_max_fun, the reference's own :445-473 built from
+the route's spline and speed limits): an arbitrary Python callable cannot be evaluated on the device and
+raises TypeError.  `optimize_full_trajectory(route, max_chunk_size=20)` restates the chunked receding-horizon
+loop (:419-559) and ends with reference_trajectory_check (:557).  Route acquisition (path_planning.py,
+GraphHopper over HTTP) is out of scope: routes.py builds the route from local way-points.
+"""
+import math
+
+import numpy as np
+
+import mpcplan
+from sanity_checks import reference_trajectory_check
+
+SQP_ITERS = 100
+
+
+class TrajectoryOptimizer:
+    """trajectory_planning.py:8-391; the solve runs on the GPU (mpcplan.Planner)."""
+
+    def __init__(self, horizon=None, N=None, dt=None, w_y=10.0, w_s=10.0, w_u=0.1, w_slack=100.0, device=0):
+        self.T = horizon
+        self.N = N
+        self.dt = dt
+        self.w_y = float(w_y)
+        self.w_s = float(w_s)
+        self.w_u = float(w_u)
+        self.w_slack = float(w_slack)
+        self.u_min = np.array([-0.6, -5.0])
+        self.u_max = np.array([0.6, 4.0])
+        self.k_min = -0.8
+        self.k_max = 0.8
+        self.a_max = 6.0
+        self.device = device
+        self.last_status = None
+        self._planners = {}
+
+    @staticmethod
+    def dynamics(x, u, k_ref):
+        """:50-89"""
+        s, d, o, k, v = x
+        u1, u2 = u
+        denom = 1 - d * k_ref
+        if abs(denom) < 1e-4:
+            denom = 1e-4 * np.sign(denom) if denom != 0 else 1e-4
+        s_dot = (v * np.cos(o)) / denom
+        return np.array([s_dot, v * np.sin(o), v * k - s_dot * k_ref, u1, u2])
+
+    def unpack(self, z):
+        """:91-113"""
+        N = self.N
+        X = z[0:(N + 1) * 5].reshape(N + 1, 5)
+        U = z[(N + 1) * 5:(N + 1) * 5 + N * 2].reshape(N, 2)
+        return X, U, z[(N + 1) * 5 + N * 2:]
+
+    @staticmethod
+    def pack(X, U, S):
+        """:115-126"""
+        return np.concatenate([X.ravel(), U.ravel(), S.ravel()])
+
+    def cost(self, z, x0, s_total):
+        """:128-170"""
+        X, U, S = self.unpack(z)
+        denom = max(1, s_total - x0[0])
+        c = 0.0
+        for k in range(self.N):
+            s_k, d_k, o_k, _, _ = X[k]
+            c += (self.w_y * (d_k ** 2 + o_k ** 2) + self.w_s * ((s_total - s_k) / denom) ** 2
+                  + self.w_u * (U[k] @ U[k]) + self.w_slack * S[k] ** 2)
+        return c
+
+    def params(self, route_vmin=0.0):
+        p = mpcplan.default_params(N=int(self.N), dt=float(self.dt), w_y=self.w_y, w_s=self.w_s, w_u=self.w_u,
+                                   w_slack=self.w_slack, u_min=self.u_min, u_max=self.u_max, k_min=self.k_min,
+                                   k_max=self.k_max, a_max=self.a_max, v_min=float(route_vmin), sqp_iters=SQP_ITERS)
+        return p
+
+    def planner(self, route, v_min=0.0):
+        key = (id(route), float(v_min))
+        pl = self._planners.get(key)
+        if pl is None:
+            pl = mpcplan.Planner(route, self.params(v_min), device=self.device)
+            self._planners[key] = pl
+        else:
+            pl.set_params(self.params(v_min))
+        return pl
+
+    def optimize(self, x0, s_target, s_total, k_ref_fun, v_min_fun, v_max_fun, is_final_chunk):
+        """:351-390 — returns (X [N+1,5], U [N,2], S [N]); the chunk's status is left in self.last_status."""
+        route = getattr(k_ref_fun, "__self__", None)
+        if route is None or getattr(v_max_fun, "__self__", None) is not route or not hasattr(route, "cx"):
+            raise TypeError("the GPU planner evaluates the route on the device: pass k_ref_fun / v_max_fun of a "
+                            "routes.Route (route.k_ref_fun, route.v_max_fun)")
+        if abs(float(s_total) - route.s_total) > 1e-9 * max(1.0, route.s_total):
+            raise ValueError("s_total must be the route's total length")
+        v_min = float(v_min_fun(x0[0]))
+        r = self.planner(route, v_min).solve_chunks(np.asarray(x0, np.float64)[None], float(s_target),
+                                                    int(bool(is_final_chunk)), int(self.N))
+        self.last_status = int(r["status"][0])
+        return r["X"][0], r["U"][0], r["S"][0]
+
+
+def optimize_full_trajectory(route, max_chunk_size=20, max_chunks=10000, device=0, verbose=False, check=True,
+                             solve_chunk=None):
+    """The chunked receding-horizon planner of trajectory_planning.py:419-559 on a routes.Route: returns
+    (X, U, S) and runs the restated reference_trajectory_check on the result (:557).  max_chunks caps the
+    loop (the reference has no cap); per-chunk statuses and horizons are left in
+    `optimize_full_trajectory.statuses` / `.horizons`.  solve_chunk(x0, s_target, is_final, N) -> (X, U, S,
+    status) replaces the GPU chunk solve (tests drive this loop with the CPU oracle)."""
+    v_min_fun = lambda s: 0                                   # :476-477
+    X_full, U_full, S_full, statuses, horizons = [], [], [], [], []
+    current_x0 = np.array([0.0, 0.0, 0.0, 0.0, 0.0])          # :486
+    s_total = route.s_total
+    if verbose:
+        print(f"Total Distance : {s_total:.2f} m")
+    remaining = s_total
+    opt = TrajectoryOptimizer(device=device)
+    n = 0
+    while remaining > 0.1 and n < max_chunks:                  # :491
+        if remaining < max_chunk_size * 2:
+            chunk_size, is_final = remaining, True
+        else:
+            chunk_size, is_final = max_chunk_size, False
+        current_s = current_x0[0]
+        s_target = current_s + chunk_size
+        if verbose:
+            print(f"==> Distance traveled --> {current_s:.2f} m ({current_s / s_total * 100:.2f}%)")
+        avg_speed = route.avg_speed_from(current_s)            # :507
+        est_time = chunk_size / avg_speed
+        horizon = est_time * 2.0
+        dt = 0.3
+        N = int(np.ceil(horizon / dt))
+        if N > mpcplan.PLAN_MAX_N:
+            raise ValueError(f"chunk horizon N={N} exceeds PLAN_MAX_N={mpcplan.PLAN_MAX_N}")
+        opt.T, opt.N, opt.dt = horizon, N, dt
+        if solve_chunk is None:
+            X, U, S = opt.optimize(current_x0, s_target, s_total, route.k_ref_fun, v_min_fun, route.v_max_fun,
+                                   is_final)
+            statuses.append(opt.last_status)
+        else:
+            X, U, S, st = solve_chunk(current_x0, s_target, is_final, N)
+            statuses.append(int(st))
+        horizons.append(N)
+        if not is_final:                                       # :523-541
+            commit = int(N / 2)
+            Xs, Us, Ss = X[:commit + 1], U[:commit], S[:commit]
+            X_full.append(Xs if not X_full else Xs[1:])
+            U_full.append(Us)
+            S_full.append(Ss)
+        else:
+            X_full.append(X[1:])
+            U_full.append(U)
+            S_full.append(S)
+        current_x0 = X_full[-1][-1]                            # :548
+        remaining = s_total - current_x0[0]
+        n += 1
+    X_final = np.concatenate(X_full, axis=0)
+    U_final = np.concatenate(U_full, axis=0)
+    S_final = np.concatenate(S_full, axis=0)
+    optimize_full_trajectory.statuses = statuses
+    optimize_full_trajectory.horizons = horizons
+    if check:
+        reference_trajectory_check(TrajectoryOptimizer(device=device), X_final, U_final, S_final, s_total)
+    for pl in opt._planners.values():
+        pl.close()
+    return X_final, U_final, S_final

@@ -87,3 +87,58 @@ def make_batch(name, B=None, seed=None, offset=0):
             obs[b, :, 1] = v[i]
         n_obs = np.full(B, 8, np.int32)
     return dict(traj=cfg["traj"], N=cfg["N"], x0=x0, obs=obs, n_obs=n_obs, max_obs=max_obs)
+
+
+# ---------------------------------------------------------------------------------------------
+# offline planner chunks: batches of independent chunk NLPs on one route
+# ---------------------------------------------------------------------------------------------
+_ROUTES = {}
+
+
+def plan_route(name="traj1"):
+    """The planner's synthetic routes (routes.py): 'traj1'..'traj3' = the global line of the committed
+    trajectory (way-points >= 8 m apart, densified to <= 5 m as path_planning does) with 50 km/h on the first
+    half and 30 km/h after; 'synth<seed>' = routes.synthetic(seed=<seed>) (1.5 km, 30/40/50 km/h bands)."""
+    if name not in _ROUTES:
+        import routes
+        if name.startswith("traj"):
+            X = loader(int(name[4:])).X_ref
+            _ROUTES[name] = routes.from_trajectory(X, bands=((0.0, 50.0), (0.5, 30.0)), min_gap=8.0, name=name)
+        elif name.startswith("synth"):
+            _ROUTES[name] = routes.synthetic(seed=int(name[5:]), name=name)
+        else:
+            raise KeyError(name)
+    return _ROUTES[name]
+
+
+def plan_batch(route, N, B, seed=0, final_frac=0.0, offset=0):
+    """B chunks at horizon N on `route`, sized by the reference's own rule (optimize_full_trajectory,
+    trajectory_planning.py:493-515: N = ceil(2 D / avg_speed / 0.3)), i.e. chunk distance D = N 0.3 avg / 2
+    with avg_speed the mean remaining speed limit.  Per chunk (default_rng(seed), one stream per field so a
+    shard is a slice): s0 ~ U(1, s_total - D - 1) (final chunks: s_target = s_total, s0 = s_total - D);
+    d0 ~ N(0, 0.05), o0 ~ N(0, 0.01), k0 = kappa(s0), v0 ~ U(0.2, 0.9) v_max(s0) (final chunks: v0 small
+    enough to stop in D at 2.5 m/s^2).  Returns dict(x0 [B,5], s_target [B], is_final [B] int32, N)."""
+    rs = [np.random.default_rng(c) for c in np.random.SeedSequence(seed).spawn(6)]
+    tot = offset + B
+    u0, nd, no, uv, uf = (rs[0].uniform(0, 1, tot), rs[1].normal(0, 0.05, tot), rs[2].normal(0, 0.01, tot),
+                          rs[3].uniform(0.2, 0.9, tot), rs[4].uniform(0, 1, tot))
+    x0 = np.empty((B, 5))
+    st = np.empty(B)
+    fin = np.zeros(B, np.int32)
+    for b in range(B):
+        i = offset + b
+        final = uf[i] < final_frac
+        s_guess = 1.0 + u0[i] * (route.s_total - 2.0)
+        D = N * 0.3 * route.avg_speed_from(s_guess) / 2.0
+        if final:
+            s0 = max(1.0, route.s_total - D)
+            target = route.s_total
+            vmax = min(route.v_max_fun(s0), np.sqrt(2.0 * 2.5 * (route.s_total - s0)))
+        else:
+            s0 = 1.0 + u0[i] * max(1e-3, route.s_total - D - 2.0)
+            target = s0 + D
+            vmax = route.v_max_fun(s0)
+        x0[b] = (s0, nd[i], no[i], route.k_ref_fun(s0), uv[i] * vmax)
+        st[b] = target
+        fin[b] = int(final)
+    return dict(x0=x0, s_target=st, is_final=fin, N=int(N))

@@ -1,0 +1,128 @@
+"""The offline planner on the GPU (libmpcplan) against the CPU oracle (oracle/plan_oracle.c),
+through the C ABI.  Parity with the reference's own chunk solve is unpinned (trajectory_planning.py is not
+importable here); the oracle is pinned by tests/test_plan_oracle.py (scipy SLSQP on the restated NLP, the
+committed planner outputs, the reference_trajectory_check goldens).
+
+Tolerances: chunks that both sides solve to convergence (status ok / frozen limits) agree to 1e-8 abs on
+X, U, S (both converge to the same KKT point to sqp_tol 1e-9); statuses agree on >= 95% of the chunks.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-8
+
+
+@pytest.fixture(scope="module")
+def env():
+    import __graft_entry__ as g
+    g.build()
+    import mpcplan
+    import plan_oracle as PO
+    import workloads as W
+    return mpcplan, PO, W
+
+
+def test_route_eval_matches_oracle(env):
+    mpcplan, PO, W = env
+    for name in ("traj1", "synth1"):
+        r = W.plan_route(name)
+        pl = mpcplan.Planner(r)
+        orc = PO.PlanOracle(r)
+        s = np.concatenate([np.linspace(-2.0, r.s_total + 2.0, 997), r.s])
+        k, dk, vm = pl.route_eval(s)
+        ko = np.array([orc.kappa(x) for x in s])
+        assert np.abs(k - ko[:, 0]).max() <= 1e-12 * (1 + np.abs(ko[:, 0]).max())
+        assert np.abs(dk - ko[:, 1]).max() <= 1e-9 * (1 + np.abs(ko[:, 1]).max())
+        assert np.array_equal(vm, np.array([orc.vmax(x) for x in s]))
+        pl.close()
+
+
+def compare(label, r, ro):
+    both = np.isin(r["status"], (0, 4)) & np.isin(ro["status"], (0, 4))
+    agree = float((r["status"] == ro["status"]).mean())
+    err = np.array([max(np.abs(r[k][b] - ro[k][b]).max() for k in ("X", "U", "S")) for b in range(len(both))])
+    print(f"{label}: B={len(both)} status agree {agree:.3f}, both converged {both.sum()}, max err {err[both].max():.1e}, "
+          f"GPU statuses {np.bincount(r['status'], minlength=5).tolist()}, oracle {np.bincount(ro['status'], minlength=5).tolist()}, "
+          f"sqp mean {r['sqp'].mean():.1f} max {r['sqp'].max()}")
+    assert agree >= 0.95, label
+    assert err[both].max() <= TOL, (label, np.flatnonzero(both & (err > TOL)))
+    return both
+
+
+@pytest.mark.parametrize("N,route", [(10, "traj1"), (20, "traj2"), (20, "synth1"), (40, "synth2")])
+def test_chunks_vs_oracle(env, N, route):
+    """>= 256 chunks per horizon N in {10, 20, 40}, a quarter of them final chunks (terminal equalities)."""
+    mpcplan, PO, W = env
+    r = W.plan_route(route)
+    wb = W.plan_batch(r, N, 256, seed=N, final_frac=0.25)
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=N))
+    g = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    o = PO.PlanOracle(r).solve_batch(PO.default_params(N=N), wb["x0"], wb["s_target"], wb["is_final"], num_threads=16)
+    both = compare(f"N={N} {route}", g, o)
+    assert both.mean() >= 0.7
+    pl.close()
+
+
+def test_mixed_horizons_one_launch(env):
+    """Per-chunk N (the receding-horizon loop's chunks differ in N): one launch over N in {8, 16, 24}; rows past a
+    chunk's N are zero, and each chunk equals its own solve at that N."""
+    mpcplan, PO, W = env
+    r = W.plan_route("synth1")
+    parts = [W.plan_batch(r, n, 40, seed=7 + n, final_frac=0.2) for n in (8, 16, 24)]
+    x0 = np.concatenate([p["x0"] for p in parts]); st = np.concatenate([p["s_target"] for p in parts])
+    fin = np.concatenate([p["is_final"] for p in parts]); N = np.repeat([8, 16, 24], 40).astype(np.int32)
+    pl = mpcplan.Planner(r)
+    g = pl.solve_chunks(x0, st, fin, N)
+    assert g["X"].shape == (120, 25, 5)
+    for i, n in enumerate((8, 16, 24)):
+        sl = slice(40 * i, 40 * i + 40)
+        assert (g["X"][sl, n + 1:] == 0).all() and (g["U"][sl, n:] == 0).all()
+        pl.set_params(mpcplan.default_params(N=n))
+        one = pl.solve_chunks(x0[sl], st[sl], fin[sl])
+        assert np.array_equal(one["X"], g["X"][sl, :n + 1]) and np.array_equal(one["status"], g["status"][sl])
+    pl.close()
+
+
+def test_device_entry_equals_host_entry(env):
+    import torch
+    mpcplan, PO, W = env
+    r = W.plan_route("traj3")
+    wb = W.plan_batch(r, 16, 100, seed=11, final_frac=0.3)
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=16))
+    h = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    x0, st, fin = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32)
+    B = 100
+    X = torch.empty((B, 17, 5), dtype=torch.float64, device=dev)
+    U = torch.empty((B, 16, 2), dtype=torch.float64, device=dev)
+    S = torch.empty((B, 16), dtype=torch.float64, device=dev)
+    o = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3)]
+    stream = torch.cuda.current_stream(dev)
+    pl.solve_chunks_device(B, 16, 0, x0.data_ptr(), st.data_ptr(), fin.data_ptr(), X.data_ptr(), U.data_ptr(),
+                           S.data_ptr(), *[a.data_ptr() for a in o], stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert np.array_equal(X.cpu().numpy(), h["X"]) and np.array_equal(U.cpu().numpy(), h["U"])
+    assert np.array_equal(o[0].cpu().numpy(), h["status"]) and np.array_equal(o[2].cpu().numpy(), h["sqp"])
+    pl.close()
+
+
+def test_full_trajectory_on_gpu_passes_reference_check(env, capsys):
+    """optimize_full_trajectory (trajectory_planning.py:419-559) with every chunk solved on the GPU: the plan
+    reaches the destination, stops, and passes the restated reference_trajectory_check (sanity_checks.py:3-75)."""
+    mpcplan, PO, W = env
+    import sanity_checks as SC
+    import trajectory_planning as TP
+    for name in ("synth1", "traj1"):
+        r = W.plan_route(name)
+        X, U, S = TP.optimize_full_trajectory(r)
+        out = capsys.readouterr().out
+        st = np.array(TP.optimize_full_trajectory.statuses)
+        q = SC.plan_check_summary(np.array([-0.6, -5.0]), np.array([0.6, 4.0]), X, U, S, r.s_total)
+        print(f"{name}: {len(st)} chunks, N {min(TP.optimize_full_trajectory.horizons)}-"
+              f"{max(TP.optimize_full_trajectory.horizons)}, statuses {np.bincount(st, minlength=5).tolist()}, "
+              f"{'passed' if q['passed'] else 'FAILED'}")
+        assert "===> Checks passed : True" in out, out
+        assert q["passed"] and np.isin(st, (0, 4)).mean() >= 0.9
