@@ -1,0 +1,1643 @@
+// plan_kernel.h — the planner's device code (one wavefront per chunk, LDS working set); included by plan.hip
+// and, with tools/plan_emu.cpp's definitions of the HIP built-ins, by the host emulation used to debug it
+// under AddressSanitizer.  See plan.hip for the design.
+#pragma once
+#include <cmath>
+#include "../../include/mpcplan.h"
+
+#ifndef PLAN_LDS_DECL
+#define PLAN_LDS_DECL extern __shared__ double lds[]
+#endif
+#ifndef PLAN_LDS_AS
+#define PLAN_LDS_AS __attribute__((address_space(3)))
+#endif
+typedef PLAN_LDS_AS double ldsd;
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int NZ = 8;             // stage variables: x (s, d, o, k, v), w (u1, u2, S)
+constexpr int NR = 11;            // rows per stage at most
+constexpr int NH = 36;            // packed symmetric 8x8
+constexpr double RHO = 1e8;       // penalty of the active rows in the equality-constrained solve
+constexpr int AL_STEPS = 4;
+constexpr int POLISH_ROUNDS = 6;
+constexpr double SHIFT0 = 1.0;
+constexpr double TAU = 0.995;
+constexpr double CYCLE_REL = 1e-6;
+constexpr double DELTA0 = 1e-6;
+constexpr double DELTA_MAX = 1e4;
+constexpr double EXACT_STEP = 0.1;
+constexpr double LS_ARMIJO = 1e-4;
+constexpr int LS_STEPS = 12;
+constexpr double LS_FULL = 1e-3;
+constexpr int LS_MEMORY = 4;
+
+enum { ROW_VMIN, ROW_VMAX, ROW_LATP, ROW_LATM, ROW_KMIN, ROW_KMAX, ROW_U1MIN, ROW_U1MAX, ROW_U2MIN, ROW_U2MAX,
+       ROW_S, ROW_STERM };
+
+struct DevRoute {
+    const double *s, *cx, *cy, *vmax;
+    int M;
+    double s_total;
+};
+
+// LDS layout of one chunk (doubles; per-stage counts times NP = Nmax + 1).  Arrays used only by the interior
+// point alias the polish's: DSA = Y, DLA = TLAM, DS = TZ (the polish runs after the interior point is done).
+struct Layout {
+    int NP;
+    int oA, oB, oC, oH, oHT, oGQ, oG, oK, oL, oEZ, oZ, oS, oLAM, oGL, oDZ, oDSA, oDLA, oDS, oDL, oMY, oMLAT, oZB,
+        oZ2, oDZV, oPI, oVLIM, oVL, oACT, oTACT, oSC;
+    int oY, oTLAM, oTZ;
+    int total;
+};
+
+__host__ __device__ Layout make_layout(int Nmax) {
+    Layout y;
+    y.NP = Nmax + 1;
+    int o = 0;
+    const int np = y.NP;
+    y.oA = o; o += 25 * np;
+    y.oB = o; o += 10 * np;          // u1, u2 columns (the slack's column is zero)
+    y.oC = o; o += 5 * np;
+    y.oH = o; o += NH * np;
+    y.oHT = o; o += NH * np;         // H + delta I + row weights (the factorisation's stage Hessian)
+    y.oGQ = o; o += NZ * np;
+    y.oG = o; o += NR * np;
+    y.oK = o; o += 15 * np;
+    y.oL = o; o += 6 * np;
+    y.oEZ = o; o += 2 * NZ * np;
+    y.oZ = o; o += NZ * np;
+    y.oS = o; o += NR * np;
+    y.oLAM = o; o += NR * np;
+    y.oGL = o; o += NZ * np;
+    y.oDZ = o; o += NZ * np;
+    y.oDSA = o; o += NR * np;
+    y.oDLA = o; o += NR * np;
+    y.oDS = o; o += NR * np;
+    y.oDL = o; o += NR * np;
+    y.oMY = o; o += 5 * np;
+    y.oMLAT = o; o += 2 * np;
+    y.oZB = o; o += NZ * np;
+    y.oZ2 = o; o += NZ * np;
+    y.oDZV = o; o += NZ * np;
+    y.oPI = o; o += 5 * np;
+    y.oVLIM = o; o += np;
+    y.oVL = o; o += np;
+    y.oACT = o; o += np;             // active-row bit masks (11 bits), stored as doubles
+    y.oTACT = o; o += np;
+    y.oSC = o; o += 16;              // scalars shared by the wave
+    y.oY = y.oDSA;
+    y.oTLAM = y.oDLA;
+    y.oTZ = y.oDS;
+    y.total = o;
+    return y;
+}
+
+// phases of the diagnostic build
+enum { PH_OTHER, PH_BUILD, PH_HESS, PH_FACTOR, PH_SOLVE, PH_IPM, PH_EQP, PH_MULT, PH_LSEARCH, PH_ROLLOUT, PH_COUNT };
+
+// scalar slots (oSC + ...)
+enum { SC_DELTA, SC_NU0, SC_NU1, SC_EM0, SC_EM1, SC_EM2, SC_EM3, SC_FLAG };
+
+// ------------------------------------------------------------------------------------------------------
+// wave reductions
+// ------------------------------------------------------------------------------------------------------
+__device__ inline double wmax(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+__device__ inline double wmin(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+__device__ inline double wsum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+__device__ inline int wsumi(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// route: k_ref_fun (:445-459) and v_max_fun (:470-473)
+// ------------------------------------------------------------------------------------------------------
+__device__ int lower_bound_d(const double* x, int n, double v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (x[m] < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+__device__ int upper_bound_d(const double* x, int n, double v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (x[m] <= v) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+// kappa(s) with d/ds and d2/ds2 (k2 may be null): s_to_t linear (searchsorted left, clipped to [1, M-1]),
+// spline piece floor(t) clipped to [0, M-2]
+__device__ double route_kappa(const DevRoute& R, double s, double* k1, double* k2) {
+    const int M = R.M;
+    int i = lower_bound_d(R.s, M, s);
+    i = i < 1 ? 1 : (i > M - 1 ? M - 1 : i);
+    const double slope = 1.0 / (R.s[i] - R.s[i - 1]);
+    const double t = slope * (s - R.s[i - 1]) + (double)(i - 1);
+    int j = (int)floor(t);
+    j = j < 0 ? 0 : (j > M - 2 ? M - 2 : j);
+    const double tau = t - (double)j;
+    const double* a = R.cx + 4 * j;
+    const double* b = R.cy + 4 * j;
+    const double x1 = (3.0 * a[0] * tau + 2.0 * a[1]) * tau + a[2], x2 = 6.0 * a[0] * tau + 2.0 * a[1], x3 = 6.0 * a[0];
+    const double y1 = (3.0 * b[0] * tau + 2.0 * b[1]) * tau + b[2], y2 = 6.0 * b[0] * tau + 2.0 * b[1], y3 = 6.0 * b[0];
+    const double num = x1 * y2 - y1 * x2;
+    const double q = x1 * x1 + y1 * y1;
+    const double sq = sqrt(q);
+    double den = q * sq + 1e-9;
+    const bool clamp = den < 1e-8;
+    if (clamp) den = 1e-8;
+    const double k = num / den;
+    if (k1) {
+        const double dnum = x1 * y3 - y1 * x3;
+        const double dden = clamp ? 0.0 : 3.0 * sq * (x1 * x2 + y1 * y2);
+        const double kt = (dnum - k * dden) / den;
+        *k1 = kt * slope;
+        if (k2) {
+            const double d2num = x2 * y3 - y2 * x3;
+            const double qd = 2.0 * (x1 * x2 + y1 * y2), qdd = 2.0 * (x2 * x2 + x1 * x3 + y2 * y2 + y1 * y3);
+            const double d2den = (clamp || sq == 0.0) ? 0.0 : 0.75 * qd * qd / sq + 1.5 * sq * qdd;
+            *k2 = (d2num - 2.0 * kt * dden - k * d2den) / den * slope * slope;
+        }
+    }
+    return k;
+}
+
+__device__ double route_vmax(const DevRoute& R, double s) {
+    const int i = upper_bound_d(R.s, R.M, s);
+    return R.vmax[i > 0 ? i - 1 : 0];
+}
+
+// ------------------------------------------------------------------------------------------------------
+// the NLP's functions (trajectory_planning.py:50-89, :128-170, :181-210) and derivatives
+// ------------------------------------------------------------------------------------------------------
+__device__ double guard_den(double den) {
+    if (fabs(den) < 1e-4) den = den > 0.0 ? 1e-4 : (den < 0.0 ? -1e-4 : 1e-4);
+    return den;
+}
+
+__device__ void dyn(const double x[5], double u1, double u2, double kr, double f[5]) {
+    const double den = guard_den(1.0 - x[1] * kr);
+    const double sd = (x[4] * cos(x[2])) / den;
+    f[0] = sd;
+    f[1] = x[4] * sin(x[2]);
+    f[2] = x[4] * x[3] - sd * kr;
+    f[3] = u1;
+    f[4] = u2;
+}
+
+__device__ void dyn_jac(const double x[5], double kr, double dk, double F[25]) {
+    const double d = x[1], o = x[2], k = x[3], v = x[4];
+    const double raw = 1.0 - d * kr;
+    const bool g = fabs(raw) < 1e-4;
+    const double den = guard_den(raw);
+    const double c = cos(o), sn = sin(o);
+    const double sd = v * c / den;
+    double ds[5];
+    ds[0] = g ? 0.0 : v * c * d * dk / (den * den);
+    ds[1] = g ? 0.0 : v * c * kr / (den * den);
+    ds[2] = -v * sn / den;
+    ds[3] = 0.0;
+    ds[4] = c / den;
+#pragma unroll
+    for (int i = 0; i < 25; ++i) F[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        F[j] = ds[j];
+        F[10 + j] = -kr * ds[j];
+    }
+    F[7] = v * c;
+    F[9] = sn;
+    F[10] += -dk * sd;
+    F[13] += v;
+    F[14] += k;
+}
+
+__device__ void hess_f(const double x[5], double kr, double k1, double k2, const double y[5], double W[25]) {
+    const double d = x[1], o = x[2], v = x[4];
+    const double raw = 1.0 - d * kr;
+    const bool gu = fabs(raw) < 1e-4;
+    const double g = 1.0 / guard_den(raw);
+    const double c = cos(o), sn = sin(o);
+    const double gs = gu ? 0.0 : d * k1 * g * g, gd = gu ? 0.0 : kr * g * g;
+    const double gss = gu ? 0.0 : d * k2 * g * g + 2.0 * d * d * k1 * k1 * g * g * g;
+    const double gsd = gu ? 0.0 : k1 * g * g + 2.0 * d * k1 * kr * g * g * g;
+    const double gdd = gu ? 0.0 : 2.0 * kr * kr * g * g * g;
+    const double ds[5] = {v * c * gs, v * c * gd, -v * sn * g, 0.0, c * g};
+    const double sd = v * c * g;
+    const double cs = y[0] - y[2] * kr;
+#pragma unroll
+    for (int i = 0; i < 25; ++i) W[i] = 0.0;
+    W[0] = cs * v * c * gss;
+    W[1] = W[5] = cs * v * c * gsd;
+    W[6] = cs * v * c * gdd;
+    W[2] = W[10] = cs * -v * sn * gs;
+    W[7] = W[11] = cs * -v * sn * gd;
+    W[12] = cs * -v * c * g;
+    W[4] = W[20] = cs * c * gs;
+    W[9] = W[21] = cs * c * gd;
+    W[14] = W[22] = cs * -sn * g;
+    W[12] += -y[1] * v * sn;
+    W[14] += y[1] * c;
+    W[22] += y[1] * c;
+    W[19] += y[2];
+    W[23] += y[2];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        W[j] += -y[2] * k1 * ds[j];
+        W[5 * j] += -y[2] * k1 * ds[j];
+    }
+    W[0] += -y[2] * sd * k2;
+}
+
+__device__ void defect(const DevRoute& R, const plan_params& P, const double xa[5], const double xb[5], double u1,
+                       double u2, double def[5]) {
+    const double h = P.dt;
+    double fa[5], fb[5], fm[5], xm[5];
+    dyn(xa, u1, u2, route_kappa(R, xa[0], nullptr, nullptr), fa);
+    dyn(xb, u1, u2, route_kappa(R, xb[0], nullptr, nullptr), fb);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) xm[i] = 0.5 * (xa[i] + xb[i]) + (h / 8.0) * (fa[i] - fb[i]);
+    dyn(xm, u1, u2, route_kappa(R, xm[0], nullptr, nullptr), fm);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) def[i] = xb[i] - (xa[i] + P.defect_sign * (h / 6.0) * (fa[i] + 4.0 * fm[i] + fb[i]));
+}
+
+// the rows of stage k (kinds in order) — the structure of build_qp in the oracle
+__device__ int stage_rows(int k, int N, int fin, int kinds[NR]) {
+    int n = 0;
+    if (!(fin && k == N)) {
+        kinds[n++] = ROW_VMIN;
+        kinds[n++] = ROW_VMAX;
+        if (k > 0) {
+            kinds[n++] = ROW_LATP;
+            kinds[n++] = ROW_LATM;
+        }
+    }
+    if (k > 0) {
+        kinds[n++] = ROW_KMIN;
+        kinds[n++] = ROW_KMAX;
+    }
+    if (k < N) {
+        kinds[n++] = ROW_U1MIN;
+        kinds[n++] = ROW_U1MAX;
+        kinds[n++] = ROW_U2MIN;
+        kinds[n++] = ROW_U2MAX;
+        kinds[n++] = ROW_S;
+    }
+    if (k == N && !fin) kinds[n++] = ROW_STERM;
+    return n;
+}
+
+// coefficients of a row over (x_k, w_k), at the SQP iterate's (k, v) of stage k
+__device__ void row_coef(int kind, bool has_w, double kb, double vb, double a[NZ]) {
+#pragma unroll
+    for (int u = 0; u < NZ; ++u) a[u] = 0.0;
+    switch (kind) {
+        case ROW_VMIN: a[4] = 1.0; a[7] = has_w ? 1.0 : 0.0; break;
+        case ROW_VMAX: a[4] = -1.0; a[7] = has_w ? -1.0 : 0.0; break;
+        case ROW_LATP: a[3] = -vb * vb; a[4] = -2.0 * kb * vb; break;
+        case ROW_LATM: a[3] = vb * vb; a[4] = 2.0 * kb * vb; break;
+        case ROW_KMIN: a[3] = 1.0; break;
+        case ROW_KMAX: a[3] = -1.0; break;
+        case ROW_U1MIN: a[5] = 1.0; break;
+        case ROW_U1MAX: a[5] = -1.0; break;
+        case ROW_U2MIN: a[6] = 1.0; break;
+        case ROW_U2MAX: a[6] = -1.0; break;
+        case ROW_S: a[7] = 1.0; break;
+        default: a[0] = 1.0; break;                              // ROW_STERM
+    }
+}
+
+// Gaussian elimination with partial pivoting on a 5x5 system with NC right-hand sides (registers)
+template <int NC>
+__device__ bool solve5(double M[25], double R[5 * NC]) {
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        int pr = c;
+        for (int i = c + 1; i < 5; ++i)
+            if (fabs(M[5 * i + c]) > fabs(M[5 * pr + c])) pr = i;
+        if (M[5 * pr + c] == 0.0) return false;
+        if (pr != c) {
+            for (int j = 0; j < 5; ++j) { const double t = M[5 * c + j]; M[5 * c + j] = M[5 * pr + j]; M[5 * pr + j] = t; }
+            for (int j = 0; j < NC; ++j) { const double t = R[NC * c + j]; R[NC * c + j] = R[NC * pr + j]; R[NC * pr + j] = t; }
+        }
+        for (int i = c + 1; i < 5; ++i) {
+            const double f = M[5 * i + c] / M[5 * c + c];
+            for (int j = c; j < 5; ++j) M[5 * i + j] -= f * M[5 * c + j];
+            for (int j = 0; j < NC; ++j) R[NC * i + j] -= f * R[NC * c + j];
+        }
+    }
+    for (int c = 4; c >= 0; --c)
+        for (int j = 0; j < NC; ++j) {
+            double v = R[NC * c + j];
+            for (int k = c + 1; k < 5; ++k) v -= M[5 * c + k] * R[NC * k + j];
+            R[NC * c + j] = v / M[5 * c + c];
+        }
+    return true;
+}
+
+__device__ bool chol3(const double H[3][3], double L[6]) {
+    if (!(H[0][0] > 0.0)) return false;
+    L[0] = sqrt(H[0][0]);
+    L[1] = H[1][0] / L[0];
+    const double d1 = H[1][1] - L[1] * L[1];
+    if (!(d1 > 0.0)) return false;
+    L[2] = sqrt(d1);
+    L[3] = H[2][0] / L[0];
+    L[4] = (H[2][1] - L[3] * L[1]) / L[2];
+    const double d2 = H[2][2] - L[3] * L[3] - L[4] * L[4];
+    if (!(d2 > 0.0)) return false;
+    L[5] = sqrt(d2);
+    return true;
+}
+
+__device__ inline void chol3_solve(const double L[6], double b[3]) {
+    const double y0 = b[0] / L[0];
+    const double y1 = (b[1] - L[1] * y0) / L[2];
+    const double y2 = (b[2] - L[3] * y0 - L[4] * y1) / L[5];
+    b[2] = y2 / L[5];
+    b[1] = (y1 - L[4] * b[2]) / L[2];
+    b[0] = (y0 - L[1] * b[1] - L[3] * b[2]) / L[0];
+}
+
+__host__ __device__ constexpr int hx(int i, int j) {   // packed index of the symmetric 8x8 (i <= j)
+    return i * NZ - (i * (i - 1)) / 2 + (j - i);
+}
+__device__ inline int hidx(int i, int j) { return i <= j ? hx(i, j) : hx(j, i); }
+
+// ------------------------------------------------------------------------------------------------------
+// the chunk: LDS working set, per-lane view
+// ------------------------------------------------------------------------------------------------------
+struct Ctx {
+    DevRoute R;
+    plan_params P;
+    Layout Y;
+    ldsd* L;            // the chunk's LDS block (explicit address space: ds_read / ds_write, never flat)
+    int ln;             // lane
+    int N, fin;
+    double x0[5], st, den;
+    double delta;       // uniform
+    double xi0[5], e[2], nu[2];
+#ifdef PLAN_PROF
+    mutable unsigned long long pt, pacc[PH_COUNT];
+    mutable int pc;
+#endif
+};
+
+// phase-time instrumentation of the diagnostic build (-DPLAN_PROF, libmpcplan_prof.so, tools/plan_phase.py):
+// the wave's time between phase switches (s_memtime), summed per phase over the chunks of a launch
+#ifdef PLAN_PROF
+__device__ unsigned long long g_plan_prof[16];
+__device__ inline int ph(const Ctx& X, int p) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    X.pacc[X.pc] += t - X.pt;
+    X.pt = t;
+    const int o = X.pc;
+    X.pc = p;
+    return o;
+}
+struct PhScope {
+    const Ctx& X;
+    int o;
+    __device__ PhScope(const Ctx& x, int p) : X(x), o(ph(x, p)) {}
+    __device__ ~PhScope() { ph(X, o); }
+};
+#define PHASE(p) PhScope ph_scope_(X, p)
+#else
+#define PHASE(p)
+#endif
+
+__device__ inline void coef_of(const Ctx& X, int k, int kind, double a[NZ]) {
+    row_coef(kind, k < X.N, X.L[X.Y.oZB + NZ * k + 3], X.L[X.Y.oZB + NZ * k + 4], a);
+}
+
+__device__ inline double row_val(const Ctx& X, int k, int j, const double a[NZ], int oz) {
+    double v = X.L[X.Y.oG + NR * k + j];
+#pragma unroll
+    for (int u = 0; u < NZ; ++u) v += a[u] * X.L[oz + NZ * k + u];
+    return v;
+}
+
+__device__ inline bool act_bit(const Ctx& X, int o, int k, int j) {
+    return (((unsigned)X.L[o + k]) >> j) & 1u;
+}
+
+__device__ inline void sync() { __syncthreads(); }
+
+// interval Jacobians at the iterate: D1 = d def / d x_{k+1}, and (when R given) the rhs [-D0 | sg h e3, e4 | -def]
+__device__ void interval_jac(const Ctx& X, const double xa[5], const double xb[5], double u1, double u2, double D1[25],
+                             double* R) {
+    const double h = X.P.dt, sg = X.P.defect_sign;
+    double dka, dkb, dkm, fa[5], fb[5], fm[5], xm[5], Fa[25], Fb[25], Fm[25];
+    const double ka = route_kappa(X.R, xa[0], &dka, nullptr);
+    const double kb = route_kappa(X.R, xb[0], &dkb, nullptr);
+    dyn(xa, u1, u2, ka, fa);
+    dyn(xb, u1, u2, kb, fb);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) xm[i] = 0.5 * (xa[i] + xb[i]) + (h / 8.0) * (fa[i] - fb[i]);
+    const double km = route_kappa(X.R, xm[0], &dkm, nullptr);
+    dyn(xm, u1, u2, km, fm);
+    dyn_jac(xa, ka, dka, Fa);
+    dyn_jac(xb, kb, dkb, Fb);
+    dyn_jac(xm, km, dkm, Fm);
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+            for (int l = 0; l < 5; ++l) {
+                const double ia = (l == j ? 0.5 : 0.0) + (h / 8.0) * Fa[5 * l + j];
+                const double ib = (l == j ? 0.5 : 0.0) - (h / 8.0) * Fb[5 * l + j];
+                m0 += Fm[5 * i + l] * ia;
+                m1 += Fm[5 * i + l] * ib;
+            }
+            if (R) R[8 * i + j] = -((i == j ? -1.0 : 0.0) - sg * (h / 6.0) * (Fa[5 * i + j] + 4.0 * m0));
+            D1[5 * i + j] = (i == j ? 1.0 : 0.0) - sg * (h / 6.0) * (4.0 * m1 + Fb[5 * i + j]);
+        }
+    if (R) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const double def = xb[i] - (xa[i] + sg * (h / 6.0) * (fa[i] + 4.0 * fm[i] + fb[i]));
+            R[8 * i + 5] = i == 3 ? sg * h : 0.0;
+            R[8 * i + 6] = i == 4 ? sg * h : 0.0;
+            R[8 * i + 7] = -def;
+        }
+    }
+}
+
+// interval k's share of the Lagrangian Hessian (-y . def_k over (x_a, x_b)) folded into stage k's Hessian
+// and gradient along x_{k+1} = A x_k + B w_k + c (A, B, c of this stage already in LDS)
+__device__ void interval_hess_fold(Ctx& X, int k, const double xa[5], const double xb[5], double u1, double u2,
+                                   const double y[5]) {
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    const double h = X.P.dt, f6 = X.P.defect_sign * h / 6.0;
+    double k1a, k2a, k1b, k2b, k1m, k2m, fa[5], fb[5], fm[5], xm[5], Fa[25], Fb[25], Fm[25];
+    const double ka = route_kappa(X.R, xa[0], &k1a, &k2a);
+    const double kb = route_kappa(X.R, xb[0], &k1b, &k2b);
+    dyn(xa, u1, u2, ka, fa);
+    dyn(xb, u1, u2, kb, fb);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) xm[i] = 0.5 * (xa[i] + xb[i]) + (h / 8.0) * (fa[i] - fb[i]);
+    const double km = route_kappa(X.R, xm[0], &k1m, &k2m);
+    dyn(xm, u1, u2, km, fm);
+    dyn_jac(xa, ka, k1a, Fa);
+    dyn_jac(xb, kb, k1b, Fb);
+    dyn_jac(xm, km, k1m, Fm);
+    double yb[5], Wm[25], Haa[25], Hab[25], Hbb[25];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v += Fm[5 * i + j] * y[i];
+        yb[j] = v;
+    }
+    hess_f(xm, km, k1m, k2m, y, Wm);
+    {
+        double WMa[25], WMb[25];
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                double va = 0.0, vb = 0.0;
+#pragma unroll
+                for (int l = 0; l < 5; ++l) {
+                    va += Wm[5 * i + l] * ((l == j ? 0.5 : 0.0) + (h / 8.0) * Fa[5 * l + j]);
+                    vb += Wm[5 * i + l] * ((l == j ? 0.5 : 0.0) - (h / 8.0) * Fb[5 * l + j]);
+                }
+                WMa[5 * i + j] = va;
+                WMb[5 * i + j] = vb;
+            }
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                double aa = 0.0, ab = 0.0, bb = 0.0;
+#pragma unroll
+                for (int l = 0; l < 5; ++l) {
+                    const double mai = (l == i ? 0.5 : 0.0) + (h / 8.0) * Fa[5 * l + i];
+                    const double mbi = (l == i ? 0.5 : 0.0) - (h / 8.0) * Fb[5 * l + i];
+                    aa += mai * WMa[5 * l + j];
+                    ab += mai * WMb[5 * l + j];
+                    bb += mbi * WMb[5 * l + j];
+                }
+                Haa[5 * i + j] = 4.0 * aa;
+                Hab[5 * i + j] = f6 * 4.0 * ab;
+                Hbb[5 * i + j] = 4.0 * bb;
+            }
+    }
+    {
+        double W[25];
+        hess_f(xa, ka, k1a, k2a, y, W);
+#pragma unroll
+        for (int i = 0; i < 25; ++i) Haa[i] += W[i];
+        hess_f(xa, ka, k1a, k2a, yb, W);
+#pragma unroll
+        for (int i = 0; i < 25; ++i) Haa[i] = f6 * (Haa[i] + 4.0 * (h / 8.0) * W[i]);
+        hess_f(xb, kb, k1b, k2b, y, W);
+#pragma unroll
+        for (int i = 0; i < 25; ++i) Hbb[i] += W[i];
+        hess_f(xb, kb, k1b, k2b, yb, W);
+#pragma unroll
+        for (int i = 0; i < 25; ++i) Hbb[i] = f6 * (Hbb[i] - 4.0 * (h / 8.0) * W[i]);
+    }
+    double T[5][NZ], c[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) T[i][j] = L[Y.oA + 25 * k + 5 * i + j];
+        T[i][5] = L[Y.oB + 10 * k + 2 * i];
+        T[i][6] = L[Y.oB + 10 * k + 2 * i + 1];
+        T[i][7] = 0.0;
+        c[i] = L[Y.oC + 5 * k + i];
+    }
+    double HbT[5][NZ], HabT[5][NZ];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) {
+            double vb = 0.0, va = 0.0;
+#pragma unroll
+            for (int l = 0; l < 5; ++l) { vb += Hbb[5 * i + l] * T[l][j]; va += Hab[5 * i + l] * T[l][j]; }
+            HbT[i][j] = vb;
+            HabT[i][j] = va;
+        }
+#pragma unroll
+    for (int i = 0; i < NZ; ++i)
+#pragma unroll
+        for (int j = i; j < NZ; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int l = 0; l < 5; ++l) v += T[l][i] * HbT[l][j];
+            if (i < 5) v += HabT[i][j];
+            if (j < 5) v += HabT[j][i];
+            if (i < 5 && j < 5) v += Haa[5 * i + j];
+            L[Y.oH + NH * k + hx(i, j)] += v;
+        }
+    double hbc[5];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        double v = 0.0;
+#pragma unroll
+        for (int m = 0; m < 5; ++m) v += Hbb[5 * l + m] * c[m];
+        hbc[l] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+        double v = 0.0;
+#pragma unroll
+        for (int l = 0; l < 5; ++l) v += T[l][i] * hbc[l];
+        if (i < 5)
+#pragma unroll
+            for (int m = 0; m < 5; ++m) v += Hab[5 * i + m] * c[m];
+        L[Y.oGQ + NZ * k + i] += v;
+    }
+}
+
+// the QP at the SQP iterate in ZB (stage-parallel); returns false (uniform) when a defect Jacobian is singular
+__device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
+    PHASE(PH_BUILD);
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    const plan_params& P = X.P;
+    const double den = X.den;
+    bool ok = true;
+    for (int k = X.ln; k <= N; k += WAVE) {
+        double x[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x[i] = L[Y.oZB + NZ * k + i];
+#pragma unroll
+        for (int i = 0; i < NH; ++i) L[Y.oH + NH * k + i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) L[Y.oGQ + NZ * k + i] = 0.0;
+        const double u1 = k < N ? L[Y.oZB + NZ * k + 5] : 0.0, u2 = k < N ? L[Y.oZB + NZ * k + 6] : 0.0;
+        const double sl = k < N ? L[Y.oZB + NZ * k + 7] : 0.0;
+        if (k < N) {
+            L[Y.oH + NH * k + hx(0, 0)] = 2.0 * P.w_s / (den * den);
+            L[Y.oH + NH * k + hx(1, 1)] = 2.0 * P.w_y;
+            L[Y.oH + NH * k + hx(2, 2)] = 2.0 * P.w_y;
+            L[Y.oH + NH * k + hx(5, 5)] = 2.0 * P.w_u;
+            L[Y.oH + NH * k + hx(6, 6)] = 2.0 * P.w_u;
+            L[Y.oH + NH * k + hx(7, 7)] = 2.0 * P.w_slack;
+            L[Y.oGQ + NZ * k + 0] = -2.0 * P.w_s * (X.R.s_total - x[0]) / (den * den);
+            L[Y.oGQ + NZ * k + 1] = 2.0 * P.w_y * x[1];
+            L[Y.oGQ + NZ * k + 2] = 2.0 * P.w_y * x[2];
+            L[Y.oGQ + NZ * k + 5] = 2.0 * P.w_u * u1;
+            L[Y.oGQ + NZ * k + 6] = 2.0 * P.w_u * u2;
+            L[Y.oGQ + NZ * k + 7] = 2.0 * P.w_slack * sl;
+            double xb[5], D1[25], R[5 * 8];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) xb[i] = L[Y.oZB + NZ * (k + 1) + i];
+            interval_jac(X, x, xb, u1, u2, D1, R);
+            if (!solve5<8>(D1, R)) {
+                ok = false;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) L[Y.oA + 25 * k + 5 * i + j] = R[8 * i + j];
+                    L[Y.oB + 10 * k + 2 * i] = R[8 * i + 5];
+                    L[Y.oB + 10 * k + 2 * i + 1] = R[8 * i + 6];
+                    L[Y.oC + 5 * k + i] = R[8 * i + 7];
+                }
+                if (exact) {
+                    double y[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) y[i] = L[Y.oMY + 5 * k + i];
+                    interval_hess_fold(X, k, x, xb, u1, u2, y);
+                }
+            }
+        }
+        int kinds[NR];
+        const int nr = stage_rows(k, N, X.fin, kinds);
+        const double kk = x[3], v = x[4];
+        for (int j = 0; j < nr; ++j) {
+            double gv = 0.0;
+            switch (kinds[j]) {
+                case ROW_VMIN: gv = v + sl - P.v_min; break;
+                case ROW_VMAX: gv = (frozen ? L[Y.oVLIM + k] : route_vmax(X.R, x[0])) - (v + sl); break;
+                case ROW_LATP: gv = P.a_max - kk * v * v; break;
+                case ROW_LATM: gv = P.a_max + kk * v * v; break;
+                case ROW_KMIN: gv = kk - P.k_min; break;
+                case ROW_KMAX: gv = P.k_max - kk; break;
+                case ROW_U1MIN: gv = u1 - P.u_min[0]; break;
+                case ROW_U1MAX: gv = P.u_max[0] - u1; break;
+                case ROW_U2MIN: gv = u2 - P.u_min[1]; break;
+                case ROW_U2MAX: gv = P.u_max[1] - u2; break;
+                case ROW_S: gv = sl; break;
+                default: gv = x[0] - X.st / 2.0; break;
+            }
+            L[Y.oG + NR * k + j] = gv;
+        }
+        if (exact && k > 0 && !(X.fin && k == N)) {
+            const double lp = L[Y.oMLAT + 2 * k], lm = L[Y.oMLAT + 2 * k + 1];
+            L[Y.oH + NH * k + hx(3, 4)] += 2.0 * v * (lp - lm);
+            L[Y.oH + NH * k + hx(4, 4)] += 2.0 * kk * (lp - lm);
+        }
+    }
+    ok = wmin(ok ? 1.0 : 0.0) > 0.0;
+    sync();
+#pragma unroll
+    for (int i = 0; i < 5; ++i) X.xi0[i] = X.x0[i] - L[Y.oZB + i];
+    X.e[0] = X.st - L[Y.oZB + NZ * N + 0];
+    X.e[1] = -L[Y.oZB + NZ * N + 4];
+    X.delta = 0.0;
+    return ok;
+}
+
+// the factorisation's stage Hessians HT = H + delta I + sum w a a' (stage-parallel); mode 0: w = lam / s
+// (interior point), 1: RHO on the TACT rows (polish)
+__device__ void stage_hess_par(Ctx& X, int mode) {
+    PHASE(PH_HESS);
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    for (int k = X.ln; k <= N; k += WAVE) {
+        double H[NH];
+#pragma unroll
+        for (int i = 0; i < NH; ++i) H[i] = L[Y.oH + NH * k + i];
+        const int nv = k < N ? NZ : 5;
+#pragma unroll
+        for (int i = 0; i < NZ; ++i)
+            if (i < nv) H[hx(i, i)] += X.delta;
+        int kinds[NR];
+        const int nr = stage_rows(k, N, X.fin, kinds);
+        for (int j = 0; j < nr; ++j) {
+            const double w = mode == 0 ? L[Y.oLAM + NR * k + j] / L[Y.oS + NR * k + j] : (act_bit(X, Y.oTACT, k, j) ? RHO : 0.0);
+            if (w == 0.0) continue;
+            double a[NZ];
+            coef_of(X, k, kinds[j], a);
+#pragma unroll
+            for (int u = 0; u < NZ; ++u)
+#pragma unroll
+                for (int v = u; v < NZ; ++v) H[hx(u, v)] += w * a[u] * a[v];
+        }
+#pragma unroll
+        for (int i = 0; i < NH; ++i) L[Y.oHT + NH * k + i] = H[i];
+    }
+}
+
+// LQ solve (lane 0) with zero initial state and homogeneous dynamics: stage linear terms at ogl -> odz
+__device__ void solve_core(const Ctx& X, int ogl, int odz) {
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    double p[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) p[i] = L[ogl + NZ * N + i];
+    for (int k = N - 1; k >= 0; --k) {
+        double h[3], Lc[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Lc[i] = L[Y.oL + 6 * k + i];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            double v = L[ogl + NZ * k + 5 + i];
+#pragma unroll
+            for (int l = 0; l < 5; ++l) v += L[Y.oB + 10 * k + 2 * l + i] * p[l];
+            h[i] = v;
+        }
+        h[2] = L[ogl + NZ * k + 7];
+        double t[3] = {-h[0], -h[1], -h[2]};
+        chol3_solve(Lc, t);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = t[i];
+        if (k > 0) {
+            double pn[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                double v = L[ogl + NZ * k + i];
+#pragma unroll
+                for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + i] * p[l];
+#pragma unroll
+                for (int l = 0; l < 3; ++l) v += L[Y.oK + 15 * k + 5 * l + i] * h[l];
+                pn[i] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) p[i] = pn[i];
+        }
+    }
+    double x[5] = {0, 0, 0, 0, 0};
+    for (int k = 0; k < N; ++k) {
+        double w[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double v = L[odz + NZ * k + 5 + i];
+#pragma unroll
+            for (int l = 0; l < 5; ++l) v += L[Y.oK + 15 * k + 5 * i + l] * x[l];
+            w[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) L[odz + NZ * k + i] = x[i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = w[i];
+        double xn[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            double v = 0.0;
+#pragma unroll
+            for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * i + l] * x[l];
+#pragma unroll
+            for (int l = 0; l < 2; ++l) v += L[Y.oB + 10 * k + 2 * i + l] * w[l];
+            xn[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x[i] = xn[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) L[odz + NZ * N + i] = x[i];
+#pragma unroll
+    for (int i = 5; i < NZ; ++i) L[odz + NZ * N + i] = 0.0;
+}
+
+// Riccati factorisation (lane 0) of the HT stage Hessians; false when a control pivot is not positive
+__device__ bool factor_serial(const Ctx& X) {
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    double P[25];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) P[5 * i + j] = L[Y.oHT + NH * N + hidx(i, j)];
+    for (int k = N - 1; k >= 0; --k) {
+        double A[25], Bm[10], PA[25], PB[10], Hww[3][3], Hwx[15], Lc[6], H[NH];
+#pragma unroll
+        for (int i = 0; i < NH; ++i) H[i] = L[Y.oHT + NH * k + i];
+#pragma unroll
+        for (int i = 0; i < 25; ++i) A[i] = L[Y.oA + 25 * k + i];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) Bm[i] = L[Y.oB + 10 * k + i];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int l = 0; l < 5; ++l) v += P[5 * i + l] * A[5 * l + j];
+                PA[5 * i + j] = v;
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                double v = 0.0;
+#pragma unroll
+                for (int l = 0; l < 5; ++l) v += P[5 * i + l] * Bm[2 * l + j];
+                PB[2 * i + j] = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                double v = H[hidx(5 + i, 5 + j)];
+                if (i < 2 && j < 2)
+#pragma unroll
+                    for (int l = 0; l < 5; ++l) v += Bm[2 * l + i] * PB[2 * l + j];
+                Hww[i][j] = v;
+            }
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                double v = H[hidx(5 + i, j)];
+                if (i < 2)
+#pragma unroll
+                    for (int l = 0; l < 5; ++l) v += Bm[2 * l + i] * PA[5 * l + j];
+                Hwx[5 * i + j] = v;
+            }
+        }
+        if (!chol3(Hww, Lc)) return false;
+        double K[15];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            double col[3] = {-Hwx[j], -Hwx[5 + j], -Hwx[10 + j]};
+            chol3_solve(Lc, col);
+            K[j] = col[0];
+            K[5 + j] = col[1];
+            K[10 + j] = col[2];
+        }
+#pragma unroll
+        for (int i = 0; i < 15; ++i) L[Y.oK + 15 * k + i] = K[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) L[Y.oL + 6 * k + i] = Lc[i];
+        if (k > 0) {
+            double Pn[25];
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    double v = H[hidx(i, j)];
+#pragma unroll
+                    for (int l = 0; l < 5; ++l) v += A[5 * l + i] * PA[5 * l + j];
+#pragma unroll
+                    for (int l = 0; l < 3; ++l) v += Hwx[5 * l + i] * K[5 * l + j];
+                    Pn[5 * i + j] = v;
+                }
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+#pragma unroll
+                for (int j = 0; j < 5; ++j) P[5 * i + j] = 0.5 * (Pn[5 * i + j] + Pn[5 * j + i]);
+        }
+    }
+    if (X.fin) {
+        for (int c = 0; c < 2; ++c) {
+            for (int k = 0; k <= N; ++k)
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) L[Y.oGL + NZ * k + i] = 0.0;
+            L[Y.oGL + NZ * N + (c == 0 ? 0 : 4)] = 1.0;
+            solve_core(X, Y.oGL, Y.oDZ);
+            for (int k = 0; k <= N; ++k)
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) L[Y.oEZ + 2 * NZ * k + NZ * c + i] = L[Y.oDZ + NZ * k + i];
+        }
+        const double e0 = L[Y.oEZ + 2 * NZ * N + 0], e1 = L[Y.oEZ + 2 * NZ * N + NZ + 0];
+        const double e2 = L[Y.oEZ + 2 * NZ * N + 4], e3 = L[Y.oEZ + 2 * NZ * N + NZ + 4];
+        L[Y.oSC + SC_EM0] = e0;
+        L[Y.oSC + SC_EM1] = e1;
+        L[Y.oSC + SC_EM2] = e2;
+        L[Y.oSC + SC_EM3] = e3;
+        const double det = e0 * e3 - e1 * e2;
+        if (!(fabs(det) > 0.0) || !isfinite(det)) return false;
+    }
+    return true;
+}
+
+// factorisation with the regularisation raised until the pivots are positive (uniform result)
+__device__ bool factor_reg(Ctx& X, int mode) {
+    for (;;) {
+        stage_hess_par(X, mode);
+        sync();
+        {
+            PHASE(PH_FACTOR);
+            if (X.ln == 0) X.L[X.Y.oSC + SC_FLAG] = factor_serial(X) ? 1.0 : 0.0;
+            sync();
+        }
+        const bool ok = X.L[X.Y.oSC + SC_FLAG] != 0.0;
+        sync();
+        if (ok) return true;
+        if (X.delta >= DELTA_MAX) return false;
+        X.delta = X.delta > 0.0 ? 10.0 * X.delta : DELTA0;
+    }
+}
+
+// full solve (GL filled and synced): DZ; meets E dz_N = rE exactly (final chunk); X.nu = terminal forces
+__device__ void solve(Ctx& X, const double rE[2]) {
+    PHASE(PH_SOLVE);
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    const int N = X.N;
+    if (X.ln == 0) {
+        solve_core(X, Y.oGL, Y.oDZ);
+        double n0 = 0.0, n1 = 0.0;
+        if (X.fin) {
+            const double b0 = rE[0] - L[Y.oDZ + NZ * N + 0], b1 = rE[1] - L[Y.oDZ + NZ * N + 4];
+            const double e0 = L[Y.oSC + SC_EM0], e1 = L[Y.oSC + SC_EM1], e2 = L[Y.oSC + SC_EM2], e3 = L[Y.oSC + SC_EM3];
+            const double det = e0 * e3 - e1 * e2;
+            n0 = (b0 * e3 - e1 * b1) / det;
+            n1 = (e0 * b1 - e2 * b0) / det;
+        }
+        L[Y.oSC + SC_NU0] = n0;
+        L[Y.oSC + SC_NU1] = n1;
+    }
+    sync();
+    X.nu[0] = L[Y.oSC + SC_NU0];
+    X.nu[1] = L[Y.oSC + SC_NU1];
+    if (X.fin)
+        for (int k = X.ln; k <= N; k += WAVE)
+#pragma unroll
+            for (int i = 0; i < NZ; ++i)
+                L[Y.oDZ + NZ * k + i] += X.nu[0] * L[Y.oEZ + 2 * NZ * k + i] + X.nu[1] * L[Y.oEZ + 2 * NZ * k + NZ + i];
+    sync();
+}
+
+// dynamics-feasible start at oz (lane 0): dx_0 = xi0, dw = 0
+__device__ void rollout(const Ctx& X, int oz) {
+    PHASE(PH_ROLLOUT);
+    if (X.ln == 0) {
+        const int N = X.N;
+        ldsd* L = X.L;
+        const Layout& Y = X.Y;
+        double x[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x[i] = X.xi0[i];
+        for (int k = 0; k <= N; ++k) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) L[oz + NZ * k + i] = x[i];
+#pragma unroll
+            for (int i = 5; i < NZ; ++i) L[oz + NZ * k + i] = 0.0;
+            if (k == N) break;
+            double xn[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                double v = L[Y.oC + 5 * k + i];
+#pragma unroll
+                for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * i + l] * x[l];
+                xn[i] = v;
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) x[i] = xn[i];
+        }
+    }
+    sync();
+}
+
+// gradient of the QP objective 1/2 z'(H + delta I)z + gq'z at stage k
+__device__ void grad_f(const Ctx& X, int k, int oz, double g[NZ]) {
+    const int nv = k < X.N ? NZ : 5;
+    double z[NZ], H[NH];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) z[i] = X.L[oz + NZ * k + i];
+#pragma unroll
+    for (int i = 0; i < NH; ++i) H[i] = X.L[X.Y.oH + NH * k + i];
+#pragma unroll
+    for (int i = 0; i < NZ; ++i) {
+        double v = X.L[X.Y.oGQ + NZ * k + i] + (i < nv ? X.delta * z[i] : 0.0);
+#pragma unroll
+        for (int j = 0; j < NZ; ++j) v += H[hidx(i, j)] * z[j];
+        g[i] = i < nv ? v : 0.0;
+    }
+}
+
+// equality-constrained QP on the TACT rows (estimates TLAM), solution into TZ / TLAM; 0 = KKT-consistent,
+// > 0 = offending rows (flipped in TACT), -1 = breakdown (uniform)
+__device__ int eqp(Ctx& X, double scale) {
+    PHASE(PH_EQP);
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    for (int k = X.ln; k <= N; k += WAVE)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) L[Y.oY + NR * k + j] = act_bit(X, Y.oTACT, k, j) ? L[Y.oTLAM + NR * k + j] : 0.0;
+    sync();
+    if (!factor_reg(X, 1)) return -1;
+    rollout(X, Y.oTZ);
+    for (int it = 0; it < AL_STEPS; ++it) {
+        for (int k = X.ln; k <= N; k += WAVE) {
+            double g[NZ];
+            grad_f(X, k, Y.oTZ, g);
+            int kinds[NR];
+            const int nr = stage_rows(k, N, X.fin, kinds);
+            for (int j = 0; j < nr; ++j) {
+                if (!act_bit(X, Y.oTACT, k, j)) continue;
+                double a[NZ];
+                coef_of(X, k, kinds[j], a);
+                const double f = RHO * row_val(X, k, j, a, Y.oTZ) - L[Y.oY + NR * k + j];
+#pragma unroll
+                for (int u = 0; u < NZ; ++u) g[u] += f * a[u];
+            }
+#pragma unroll
+            for (int u = 0; u < NZ; ++u) L[Y.oGL + NZ * k + u] = g[u];
+        }
+        sync();
+        const double rE[2] = {X.e[0] - L[Y.oTZ + NZ * N + 0], X.e[1] - L[Y.oTZ + NZ * N + 4]};
+        solve(X, rE);
+        for (int k = X.ln; k <= N; k += WAVE) {
+#pragma unroll
+            for (int u = 0; u < NZ; ++u) L[Y.oTZ + NZ * k + u] += L[Y.oDZ + NZ * k + u];
+            int kinds[NR];
+            const int nr = stage_rows(k, N, X.fin, kinds);
+            for (int j = 0; j < nr; ++j)
+                if (act_bit(X, Y.oTACT, k, j)) {
+                    double a[NZ];
+                    coef_of(X, k, kinds[j], a);
+                    L[Y.oY + NR * k + j] -= RHO * row_val(X, k, j, a, Y.oTZ);
+                }
+        }
+        sync();
+    }
+    double fin = 1.0;
+    int bad = 0;
+    const double tr = 1e-9 * scale, tl = 1e-9 * scale;
+    for (int k = X.ln; k <= N; k += WAVE) {
+#pragma unroll
+        for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oTZ + NZ * k + u]) ? fin : 0.0;
+        int kinds[NR];
+        const int nr = stage_rows(k, N, X.fin, kinds);
+        unsigned mask = (unsigned)L[Y.oTACT + k];
+        for (int j = 0; j < nr; ++j) {
+            double a[NZ];
+            coef_of(X, k, kinds[j], a);
+            const double rv = row_val(X, k, j, a, Y.oTZ);
+            if ((mask >> j) & 1u) {
+                const double y = L[Y.oY + NR * k + j];
+                L[Y.oTLAM + NR * k + j] = y;
+                if (y < -tl || fabs(rv) > tr) { mask &= ~(1u << j); ++bad; }
+            } else {
+                L[Y.oTLAM + NR * k + j] = 0.0;
+                if (rv < -tr) { mask |= 1u << j; ++bad; }
+            }
+        }
+        L[Y.oTACT + k] = (double)mask;
+    }
+    fin = wmin(fin);
+    bad = wsumi(bad);
+    sync();
+    if (fin == 0.0) return -1;
+    return bad;
+}
+
+// Mehrotra predictor-corrector interior point; solution in Z, S, LAM; 0 converged, 1 cap, -1 breakdown
+__device__ int ipm(Ctx& X, int* iters) {
+    PHASE(PH_IPM);
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    rollout(X, Y.oZ);
+    int m = 0;
+    for (int k = X.ln; k <= N; k += WAVE) {
+        int kinds[NR];
+        const int nr = stage_rows(k, N, X.fin, kinds);
+        for (int j = 0; j < nr; ++j) {
+            double a[NZ];
+            coef_of(X, k, kinds[j], a);
+            const double rv = row_val(X, k, j, a, Y.oZ);
+            L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
+            L[Y.oLAM + NR * k + j] = 1.0;
+            ++m;
+        }
+    }
+    m = wsumi(m);
+    sync();
+    double phi = 1.0;
+    int it = 0, rc = 1;
+    for (; it < X.P.max_iter; ++it) {
+        double mu = 0.0;
+        for (int k = X.ln; k <= N; k += WAVE) {
+            int kinds[NR];
+            const int nr = stage_rows(k, N, X.fin, kinds);
+            for (int j = 0; j < nr; ++j) mu += L[Y.oS + NR * k + j] * L[Y.oLAM + NR * k + j];
+        }
+        mu = wsum(mu) / m;
+        if (!isfinite(mu)) { rc = -1; break; }
+        if (mu <= X.P.tol && phi <= 1e-12) { rc = 0; break; }
+        if (!factor_reg(X, 0)) { rc = -1; break; }
+        const double rE[2] = {X.e[0] - L[Y.oZ + NZ * N + 0], X.e[1] - L[Y.oZ + NZ * N + 4]};
+        for (int pass = 0; pass < 2; ++pass) {
+            double sigma_mu = 0.0;
+            if (pass == 1) {
+                double am = 1.0;
+                for (int k = X.ln; k <= N; k += WAVE) {
+                    int kinds[NR];
+                    const int nr = stage_rows(k, N, X.fin, kinds);
+                    for (int j = 0; j < nr; ++j) {
+                        const double dsa = L[Y.oDSA + NR * k + j], dla = L[Y.oDLA + NR * k + j];
+                        if (dsa < 0.0) am = fmin(am, -L[Y.oS + NR * k + j] / dsa);
+                        if (dla < 0.0) am = fmin(am, -L[Y.oLAM + NR * k + j] / dla);
+                    }
+                }
+                am = wmin(am);
+                double mua = 0.0;
+                for (int k = X.ln; k <= N; k += WAVE) {
+                    int kinds[NR];
+                    const int nr = stage_rows(k, N, X.fin, kinds);
+                    for (int j = 0; j < nr; ++j)
+                        mua += (L[Y.oS + NR * k + j] + am * L[Y.oDSA + NR * k + j]) *
+                               (L[Y.oLAM + NR * k + j] + am * L[Y.oDLA + NR * k + j]);
+                }
+                mua = wsum(mua) / m;
+                const double ratio = mua / mu;
+                sigma_mu = ratio * ratio * ratio * mu;
+            }
+            for (int k = X.ln; k <= N; k += WAVE) {
+                double g[NZ];
+                grad_f(X, k, Y.oZ, g);
+                int kinds[NR];
+                const int nr = stage_rows(k, N, X.fin, kinds);
+                for (int j = 0; j < nr; ++j) {
+                    double a[NZ];
+                    coef_of(X, k, kinds[j], a);
+                    const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
+                    double rs = -s * l;
+                    if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
+                    const double rp = row_val(X, k, j, a, Y.oZ) - s;
+                    const double f = l + (rs - l * rp) / s;
+#pragma unroll
+                    for (int u = 0; u < NZ; ++u) g[u] -= f * a[u];
+                }
+#pragma unroll
+                for (int u = 0; u < NZ; ++u) L[Y.oGL + NZ * k + u] = g[u];
+            }
+            sync();
+            solve(X, rE);
+            const int ods = pass == 0 ? Y.oDSA : Y.oDS, odl = pass == 0 ? Y.oDLA : Y.oDL;
+            for (int k = X.ln; k <= N; k += WAVE) {
+                int kinds[NR];
+                const int nr = stage_rows(k, N, X.fin, kinds);
+                for (int j = 0; j < nr; ++j) {
+                    double a[NZ];
+                    coef_of(X, k, kinds[j], a);
+                    const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
+                    double rs = -s * l;
+                    if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
+                    double v = row_val(X, k, j, a, Y.oZ) - s;
+#pragma unroll
+                    for (int u = 0; u < NZ; ++u) v += a[u] * L[Y.oDZ + NZ * k + u];
+                    L[ods + NR * k + j] = v;
+                    L[odl + NR * k + j] = (rs - l * v) / s;
+                }
+            }
+            sync();
+        }
+        double amax = 1.0 / TAU, fin = 1.0;
+        for (int k = X.ln; k <= N; k += WAVE) {
+            int kinds[NR];
+            const int nr = stage_rows(k, N, X.fin, kinds);
+            for (int j = 0; j < nr; ++j) {
+                const double ds = L[Y.oDS + NR * k + j], dl = L[Y.oDL + NR * k + j];
+                if (ds < 0.0) amax = fmin(amax, -L[Y.oS + NR * k + j] / ds);
+                if (dl < 0.0) amax = fmin(amax, -L[Y.oLAM + NR * k + j] / dl);
+            }
+#pragma unroll
+            for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oDZ + NZ * k + u]) ? fin : 0.0;
+        }
+        amax = wmin(amax);
+        fin = wmin(fin);
+        const double alpha = fmin(1.0, TAU * amax);
+        if (!isfinite(alpha) || fin == 0.0) { rc = -1; break; }
+        for (int k = X.ln; k <= N; k += WAVE) {
+#pragma unroll
+            for (int u = 0; u < NZ; ++u) L[Y.oZ + NZ * k + u] += alpha * L[Y.oDZ + NZ * k + u];
+            int kinds[NR];
+            const int nr = stage_rows(k, N, X.fin, kinds);
+            for (int j = 0; j < nr; ++j) {
+                L[Y.oS + NR * k + j] += alpha * L[Y.oDS + NR * k + j];
+                L[Y.oLAM + NR * k + j] += alpha * L[Y.oDL + NR * k + j];
+            }
+        }
+        sync();
+        phi *= 1.0 - alpha;
+    }
+    sync();
+    *iters = it;
+    return rc;
+}
+
+// copy the polish result (TZ, TLAM, TACT) to the solution (Z, LAM, ACT)
+__device__ void accept_polish(const Ctx& X, bool with_act) {
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    for (int k = X.ln; k <= X.N; k += WAVE) {
+#pragma unroll
+        for (int u = 0; u < NZ; ++u) L[Y.oZ + NZ * k + u] = L[Y.oTZ + NZ * k + u];
+#pragma unroll
+        for (int j = 0; j < NR; ++j) L[Y.oLAM + NR * k + j] = L[Y.oTLAM + NR * k + j];
+        if (with_act) L[Y.oACT + k] = L[Y.oTACT + k];
+    }
+    sync();
+}
+
+// interior-point classification (s < lam) of stage k as a bit mask
+__device__ double ipm_mask(const Ctx& X, int k) {
+    int kinds[NR];
+    const int nr = stage_rows(k, X.N, X.fin, kinds);
+    unsigned m = 0;
+    for (int j = 0; j < nr; ++j)
+        if (X.L[X.Y.oS + NR * k + j] < X.L[X.Y.oLAM + NR * k + j]) m |= 1u << j;
+    return (double)m;
+}
+
+// one QP: 0 solved (KKT point), 1 interior-point answer without a certified polish, -1 failure (uniform)
+__device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    double scale = 1.0;
+    for (int k = X.ln; k <= N; k += WAVE) {
+        int kinds[NR];
+        const int nr = stage_rows(k, N, X.fin, kinds);
+        for (int j = 0; j < nr; ++j) scale = fmax(scale, fabs(L[Y.oG + NR * k + j]));
+    }
+    scale = wmax(scale);
+    *iters = 0;
+    if (have_cls) {
+        for (int k = X.ln; k <= N; k += WAVE) {
+            L[Y.oTACT + k] = L[Y.oACT + k];
+#pragma unroll
+            for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
+        }
+        sync();
+        if (eqp(X, scale) == 0) {
+            accept_polish(X, false);
+            return 0;
+        }
+    }
+    const int rc = ipm(X, iters);
+    if (rc < 0) return -1;
+    const double nu_ipm[2] = {X.nu[0], X.nu[1]};
+    for (int k = X.ln; k <= N; k += WAVE) {
+        L[Y.oTACT + k] = ipm_mask(X, k);
+#pragma unroll
+        for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
+    }
+    sync();
+    for (int round = 0; round < POLISH_ROUNDS; ++round) {
+        const int bad = eqp(X, scale);
+        if (bad < 0) break;
+        if (bad == 0) {
+            accept_polish(X, true);
+            return 0;
+        }
+    }
+    for (int k = X.ln; k <= N; k += WAVE) L[Y.oACT + k] = ipm_mask(X, k);
+    sync();
+    X.nu[0] = nu_ipm[0];
+    X.nu[1] = nu_ipm[1];
+    return rc == 0 ? 1 : -1;
+}
+
+// NLP multipliers from the QP solution (oracle multipliers()): MY, MLAT
+__device__ void multipliers(Ctx& X) {
+    PHASE(PH_MULT);
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    // stage gradients of the Lagrangian minus the rows (x part) into GL; lateral multipliers
+    for (int k = X.ln; k <= N; k += WAVE) {
+        double g[NZ];
+        grad_f(X, k, Y.oZ, g);
+        int kinds[NR];
+        const int nr = stage_rows(k, N, X.fin, kinds);
+        L[Y.oMLAT + 2 * k] = 0.0;
+        L[Y.oMLAT + 2 * k + 1] = 0.0;
+        for (int j = 0; j < nr; ++j) {
+            double a[NZ];
+            coef_of(X, k, kinds[j], a);
+            const double l = L[Y.oLAM + NR * k + j];
+#pragma unroll
+            for (int u = 0; u < NZ; ++u) g[u] -= l * a[u];
+            if (kinds[j] == ROW_LATP) L[Y.oMLAT + 2 * k] = l;
+            if (kinds[j] == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) L[Y.oGL + NZ * k + u] = g[u];
+    }
+    sync();
+    // co-states (lane 0): PI[k] = pi_{k+1}
+    if (X.ln == 0) {
+        double pi[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) pi[i] = L[Y.oGL + NZ * N + i];
+        if (X.fin) {
+            pi[0] += X.nu[0];
+            pi[4] += X.nu[1];
+        }
+        for (int k = N - 1; k >= 0; --k) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) L[Y.oPI + 5 * k + i] = pi[i];
+            if (k > 0) {
+                double pn[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) {
+                    double v = L[Y.oGL + NZ * k + i];
+#pragma unroll
+                    for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + i] * pi[l];
+                    pn[i] = v;
+                }
+#pragma unroll
+                for (int i = 0; i < 5; ++i) pi[i] = pn[i];
+            }
+        }
+    }
+    sync();
+    // y_k = D1_k^-T pi_{k+1} (stage-parallel; D1 at the iterate ZB)
+    for (int k = X.ln; k < N; k += WAVE) {
+        double xa[5], xb[5], D1[25], D1t[25], y[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            xa[i] = L[Y.oZB + NZ * k + i];
+            xb[i] = L[Y.oZB + NZ * (k + 1) + i];
+        }
+        interval_jac(X, xa, xb, L[Y.oZB + NZ * k + 5], L[Y.oZB + NZ * k + 6], D1, nullptr);
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) D1t[5 * i + j] = D1[5 * j + i];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) y[i] = L[Y.oPI + 5 * k + i];
+        const bool ok = solve5<1>(D1t, y);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) L[Y.oMY + 5 * k + i] = ok ? y[i] : 0.0;
+    }
+    sync();
+}
+
+// the NLP's cost (:128-170) and L1 violation at ZB + alpha * DZV (stage-parallel, reduced)
+__device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
+    PHASE(PH_LSEARCH);
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    const plan_params& P = X.P;
+    auto zv = [&](int k, int i) { return L[Y.oZB + NZ * k + i] + (alpha != 0.0 ? alpha * L[Y.oDZV + NZ * k + i] : 0.0); };
+    double c = 0.0, v = 0.0;
+    if (X.ln == 0)
+        for (int i = 0; i < 5; ++i) v += fabs(zv(0, i) - X.x0[i]);
+    for (int k = X.ln; k <= N; k += WAVE) {
+        double x[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x[i] = zv(k, i);
+        const double u1 = k < N ? zv(k, 5) : 0.0, u2 = k < N ? zv(k, 6) : 0.0, sl = k < N ? zv(k, 7) : 0.0;
+        if (k < N) {
+            const double e = (X.R.s_total - x[0]) / X.den;
+            c += P.w_y * (x[1] * x[1] + x[2] * x[2]) + P.w_s * e * e + P.w_u * (u1 * u1 + u2 * u2) + P.w_slack * (sl * sl);
+            double xb[5], def[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) xb[i] = zv(k + 1, i);
+            defect(X.R, P, x, xb, u1, u2, def);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) v += fabs(def[i]);
+        }
+        const double kk = x[3], vv = x[4];
+        double g[12];
+        int n = 0;
+        if (!(X.fin && k == N)) {
+            g[n++] = vv + sl - P.v_min;
+            g[n++] = L[Y.oVL + k] - (vv + sl);
+            if (k > 0) {
+                g[n++] = P.a_max - kk * vv * vv;
+                g[n++] = P.a_max + kk * vv * vv;
+            }
+        }
+        if (k > 0) {
+            g[n++] = kk - P.k_min;
+            g[n++] = P.k_max - kk;
+        }
+        if (k < N) {
+            g[n++] = u1 - P.u_min[0];
+            g[n++] = P.u_max[0] - u1;
+            g[n++] = u2 - P.u_min[1];
+            g[n++] = P.u_max[1] - u2;
+            g[n++] = sl;
+        }
+        if (k == N && !X.fin) g[n++] = x[0] - X.st / 2.0;
+        for (int j = 0; j < n; ++j) v += g[j] < 0.0 ? -g[j] : 0.0;
+        if (k == N && X.fin) v += fabs(x[0] - X.st) + fabs(x[4]);
+    }
+    *f = wsum(c);
+    *viol = wsum(v);
+}
+
+__device__ double cost_dir(const Ctx& X) {
+    PHASE(PH_LSEARCH);
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    const plan_params& P = X.P;
+    double v = 0.0;
+    for (int k = X.ln; k < N; k += WAVE) {
+        v += 2.0 * P.w_y * (L[Y.oZB + NZ * k + 1] * L[Y.oDZV + NZ * k + 1] + L[Y.oZB + NZ * k + 2] * L[Y.oDZV + NZ * k + 2]);
+        v += -2.0 * P.w_s * (X.R.s_total - L[Y.oZB + NZ * k]) / (X.den * X.den) * L[Y.oDZV + NZ * k];
+        v += 2.0 * P.w_u * (L[Y.oZB + NZ * k + 5] * L[Y.oDZV + NZ * k + 5] + L[Y.oZB + NZ * k + 6] * L[Y.oDZV + NZ * k + 6]);
+        v += 2.0 * P.w_slack * L[Y.oZB + NZ * k + 7] * L[Y.oDZV + NZ * k + 7];
+    }
+    return wsum(v);
+}
+
+struct KArgs {
+    DevRoute R;
+    plan_params P;
+    int B, Nmax, Nfixed;
+    const int* N;
+    const double *x0, *st;
+    const int* fin;
+    double *X, *U, *S;
+    int *status, *iters, *sqp;
+};
+
+__global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
+    PLAN_LDS_DECL;
+    const int b = blockIdx.x;
+    Ctx X;
+    X.R = a.R;
+    X.P = a.P;
+    X.Y = make_layout(a.Nmax);
+    X.L = (ldsd*)lds;
+    X.ln = threadIdx.x;
+    X.N = a.N ? a.N[b] : a.Nfixed;
+    const int N = X.N;
+    X.fin = a.fin ? (a.fin[b] != 0) : 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) X.x0[i] = a.x0[5 * (size_t)b + i];
+    X.st = a.st[b];
+    X.den = fmax(1.0, a.R.s_total - X.x0[0]);
+    X.nu[0] = X.nu[1] = 0.0;
+    X.delta = 0.0;
+#ifdef PLAN_PROF
+    for (int i = 0; i < PH_COUNT; ++i) X.pacc[i] = 0;
+    X.pc = PH_OTHER;
+    X.pt = __builtin_amdgcn_s_memtime();
+#endif
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    // initial guess (:357-376)
+    const double dss = (X.st - X.x0[0]) / N;
+    for (int k = X.ln; k <= N; k += WAVE) {
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) L[Y.oZB + NZ * k + i] = 0.0;
+        L[Y.oZB + NZ * k + 0] = k == N ? X.st : X.x0[0] + k * dss;
+        L[Y.oZB + NZ * k + 4] = X.fin ? (k == N ? 0.0 : X.x0[4] + k * ((0.0 - X.x0[4]) / N)) : X.x0[4];
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) L[Y.oZ2 + NZ * k + i] = L[Y.oZB + NZ * k + i];
+    }
+    sync();
+    int status = PLAN_NOT_CONVERGED, total = 0, nq = 0, since = 0;
+    bool have_cls = false, frozen = false;
+    double last = INFINITY, mu_m = 0.0, hf[LS_MEMORY], hv[LS_MEMORY];
+    int nh = 0;
+    for (int it = 0; it < a.P.sqp_iters; ++it, ++since) {
+        bool exact = last <= EXACT_STEP;
+        int rc = -1;
+        for (;;) {
+            if (!build_qp(X, frozen, exact)) { rc = -2; break; }
+            int ni = 0;
+            rc = qp_solve(X, have_cls, &ni);
+            total += ni;
+            if (rc >= 0 || !exact) break;
+            exact = false;
+        }
+        ++nq;
+        if (rc == -2) { status = PLAN_NUMERICAL; break; }
+        if (rc < 0) { status = PLAN_QP_FAILED; break; }
+        have_cls = true;
+        multipliers(X);
+        double full = 0.0, mu_l = 0.0;
+        for (int k = X.ln; k <= N; k += WAVE) {
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+                const double d = (k < N || i < 5) ? L[Y.oZ + NZ * k + i] : 0.0;
+                L[Y.oDZV + NZ * k + i] = d;
+                full = fmax(full, fabs(d));
+            }
+            if (k < N)
+#pragma unroll
+                for (int i = 0; i < 5; ++i) mu_l = fmax(mu_l, 2.0 * fabs(L[Y.oMY + 5 * k + i]));
+            int kinds[NR];
+            const int nr = stage_rows(k, N, X.fin, kinds);
+            for (int j = 0; j < nr; ++j) mu_l = fmax(mu_l, 2.0 * fabs(L[Y.oLAM + NR * k + j]));
+        }
+        full = wmax(full);
+        mu_m = fmax(mu_m, wmax(mu_l));
+        if (X.fin) mu_m = fmax(mu_m, 2.0 * fmax(fabs(X.nu[0]), fabs(X.nu[1])));
+        sync();
+        double alpha = 1.0;
+        if (full > LS_FULL) {
+            for (int k = X.ln; k <= N; k += WAVE) L[Y.oVL + k] = frozen ? L[Y.oVLIM + k] : route_vmax(X.R, L[Y.oZB + NZ * k]);
+            sync();
+            double f0, v0;
+            cost_viol(X, 0.0, &f0, &v0);
+            const double dd = cost_dir(X) - mu_m * v0;
+            hf[nh % LS_MEMORY] = f0;
+            hv[nh % LS_MEMORY] = v0;
+            ++nh;
+            double m0 = -INFINITY;
+            for (int i = 0; i < (nh < LS_MEMORY ? nh : LS_MEMORY); ++i) m0 = fmax(m0, hf[i] + mu_m * hv[i]);
+            for (int ls = 0; ls < LS_STEPS; ++ls) {
+                double f1, v1;
+                cost_viol(X, alpha, &f1, &v1);
+                if (f1 + mu_m * v1 <= m0 + LS_ARMIJO * alpha * dd || ls == LS_STEPS - 1) break;
+                alpha *= 0.5;
+            }
+        }
+        double step = 0.0, back2 = 0.0, fin = 1.0;
+        for (int k = X.ln; k <= N; k += WAVE)
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+                if (k == N && i >= 5) continue;
+                const double zo = L[Y.oZB + NZ * k + i];
+                const double zn = zo + alpha * L[Y.oDZV + NZ * k + i];
+                step = fmax(step, fabs(zn - zo));
+                back2 = fmax(back2, fabs(zn - L[Y.oZ2 + NZ * k + i]));
+                fin = isfinite(zn) ? fin : 0.0;
+            }
+        step = wmax(step);
+        back2 = wmax(back2);
+        fin = wmin(fin);
+        if (fin == 0.0) { status = PLAN_NUMERICAL; break; }
+        for (int k = X.ln; k <= N; k += WAVE)
+#pragma unroll
+            for (int i = 0; i < NZ; ++i) {
+                if (k == N && i >= 5) continue;
+                const double zo = L[Y.oZB + NZ * k + i];
+                L[Y.oZ2 + NZ * k + i] = zo;
+                L[Y.oZB + NZ * k + i] = zo + alpha * L[Y.oDZV + NZ * k + i];
+            }
+        sync();
+        last = step;
+        if (step <= a.P.sqp_tol) { status = frozen ? PLAN_FROZEN_LIMITS : PLAN_OK; break; }
+        if (since >= 2 && back2 <= CYCLE_REL * step) {
+            if (frozen) break;
+            for (int k = X.ln; k <= N; k += WAVE)
+                L[Y.oVLIM + k] = fmin(route_vmax(X.R, L[Y.oZB + NZ * k]), route_vmax(X.R, L[Y.oZ2 + NZ * k]));
+            frozen = true;
+            since = -1;
+            for (int k = X.ln; k <= N; k += WAVE)
+#pragma unroll
+                for (int i = 0; i < NZ; ++i) L[Y.oZ2 + NZ * k + i] = L[Y.oZB + NZ * k + i];
+            sync();
+        }
+    }
+    if (status == PLAN_FROZEN_LIMITS) {
+        double bad = 0.0;
+        for (int k = X.ln; k <= N; k += WAVE)
+            if (L[Y.oZB + NZ * k + 4] + (k < N ? L[Y.oZB + NZ * k + 7] : 0.0) > route_vmax(X.R, L[Y.oZB + NZ * k]) + 1e-9)
+                bad = 1.0;
+        if (wmax(bad) > 0.0) status = PLAN_NOT_CONVERGED;
+    }
+    // outputs: rows past this chunk's N are zero
+    const int Nm = a.Nmax;
+    for (int k = X.ln; k <= Nm; k += WAVE) {
+        if (a.X)
+#pragma unroll
+            for (int i = 0; i < 5; ++i) a.X[((size_t)b * (Nm + 1) + k) * 5 + i] = k <= N ? L[Y.oZB + NZ * k + i] : 0.0;
+        if (k < Nm) {
+            if (a.U) {
+                a.U[((size_t)b * Nm + k) * 2 + 0] = k < N ? L[Y.oZB + NZ * k + 5] : 0.0;
+                a.U[((size_t)b * Nm + k) * 2 + 1] = k < N ? L[Y.oZB + NZ * k + 6] : 0.0;
+            }
+            if (a.S) a.S[(size_t)b * Nm + k] = k < N ? L[Y.oZB + NZ * k + 7] : 0.0;
+        }
+    }
+    if (X.ln == 0) {
+        if (a.status) a.status[b] = status;
+        if (a.iters) a.iters[b] = total;
+        if (a.sqp) a.sqp[b] = nq;
+    }
+#ifdef PLAN_PROF
+    ph(X, PH_OTHER);
+    if (X.ln == 0) {
+        for (int i = 0; i < PH_COUNT; ++i) atomicAdd(&g_plan_prof[i], X.pacc[i]);
+        atomicAdd(&g_plan_prof[15], 1ull);
+    }
+#endif
+}
+
+__global__ void route_eval_kernel(DevRoute R, int n, const double* s, double* k, double* dk, double* vm) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double d1 = 0.0;
+    const double kv = route_kappa(R, s[i], &d1, nullptr);
+    k[i] = kv;
+    dk[i] = d1;
+    vm[i] = route_vmax(R, s[i]);
+}
+
+}  // namespace

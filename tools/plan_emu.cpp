@@ -1,0 +1,144 @@
+// plan_emu.cpp — host emulation of the planner kernel (safe-autonomous-driving-mpc_amd/csrc/plan_kernel.h) for
+// debugging it on the CPU: the kernel's own source, compiled with g++ (optionally -fsanitize=address) against
+// stand-ins for the few HIP built-ins it uses.  One workgroup = 64 POSIX threads meeting at a barrier for
+// __syncthreads and for each __shfl_xor; the chunk's LDS is an exactly-sized heap block filled with NaN, so an
+// out-of-range LDS index is an ASan report and a read of LDS never written shows up as NaN in the results.
+// Debugging aid only: not part of the product and not a parity reference (that is oracle/plan_oracle.c).
+//
+// usage: plan_emu in.bin out.bin [first_block count]     (file formats: tools/plan_emu.py)
+#include <pthread.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+using std::isfinite;
+
+#define __device__
+#define __host__
+#define __global__
+#define __launch_bounds__(x)
+#define __shared__
+
+struct EmuDim {
+    unsigned x = 0, y = 0, z = 0;
+};
+static thread_local EmuDim threadIdx, blockIdx, blockDim;
+static pthread_barrier_t g_bar;
+static double* g_lds = nullptr;
+static double g_xd[64];
+static int g_xi[64];
+
+#define PLAN_LDS_DECL double* lds = g_lds
+#define PLAN_LDS_AS
+
+static inline void __syncthreads() { pthread_barrier_wait(&g_bar); }
+static inline double __shfl_xor(double v, int o, int) {
+    g_xd[threadIdx.x] = v;
+    pthread_barrier_wait(&g_bar);
+    const double r = g_xd[threadIdx.x ^ (unsigned)o];
+    pthread_barrier_wait(&g_bar);
+    return r;
+}
+static inline int __shfl_xor(int v, int o, int) {
+    g_xi[threadIdx.x] = v;
+    pthread_barrier_wait(&g_bar);
+    const int r = g_xi[threadIdx.x ^ (unsigned)o];
+    pthread_barrier_wait(&g_bar);
+    return r;
+}
+
+#include "../safe-autonomous-driving-mpc_amd/csrc/plan_kernel.h"
+
+struct LaneArg {
+    KArgs* a;
+    int lane, block;
+};
+
+static void* lane_main(void* p) {
+    LaneArg* la = (LaneArg*)p;
+    threadIdx.x = la->lane;
+    blockIdx.x = la->block;
+    plan_chunk_kernel(*la->a);
+    return nullptr;
+}
+
+template <class T>
+static std::vector<T> rd(FILE* f, size_t n) {
+    std::vector<T> v(n);
+    if (n && fread(v.data(), sizeof(T), n, f) != n) {
+        fprintf(stderr, "short read\n");
+        exit(2);
+    }
+    return v;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        fprintf(stderr, "usage: %s in.bin out.bin [first count]\n", argv[0]);
+        return 2;
+    }
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) return 2;
+    auto hd = rd<int>(f, 5);
+    const int M = hd[0], B = hd[1], Nmax = hd[2], hasN = hd[3], hasFin = hd[4];
+    plan_params P;
+    if (fread(&P, sizeof(P), 1, f) != 1) return 2;
+    auto s = rd<double>(f, M), cx = rd<double>(f, 4 * (M - 1)), cy = rd<double>(f, 4 * (M - 1)), vm = rd<double>(f, M);
+    auto Nv = rd<int>(f, hasN ? B : 0);
+    auto x0 = rd<double>(f, 5 * (size_t)B), st = rd<double>(f, B);
+    auto fin = rd<int>(f, hasFin ? B : 0);
+    fclose(f);
+    const int first = argc > 3 ? atoi(argv[3]) : 0;
+    const int count = argc > 4 ? atoi(argv[4]) : B - first;
+    std::vector<double> X((size_t)B * (Nmax + 1) * 5, 0.0), U((size_t)B * Nmax * 2, 0.0), S((size_t)B * Nmax, 0.0);
+    std::vector<int> status(B, -1), iters(B, 0), sqp(B, 0);
+    KArgs a;
+    a.R.s = s.data();
+    a.R.cx = cx.data();
+    a.R.cy = cy.data();
+    a.R.vmax = vm.data();
+    a.R.M = M;
+    a.R.s_total = s[M - 1];
+    a.P = P;
+    a.B = B;
+    a.Nmax = Nmax;
+    a.Nfixed = P.N;
+    a.N = hasN ? Nv.data() : nullptr;
+    a.x0 = x0.data();
+    a.st = st.data();
+    a.fin = hasFin ? fin.data() : nullptr;
+    a.X = X.data();
+    a.U = U.data();
+    a.S = S.data();
+    a.status = status.data();
+    a.iters = iters.data();
+    a.sqp = sqp.data();
+    const size_t nl = (size_t)make_layout(Nmax).total;
+    pthread_barrier_init(&g_bar, nullptr, WAVE);
+    for (int b = first; b < first + count && b < B; ++b) {
+        std::vector<double> lds(nl, std::numeric_limits<double>::quiet_NaN());
+        g_lds = lds.data();
+        pthread_t th[WAVE];
+        LaneArg la[WAVE];
+        for (int l = 0; l < WAVE; ++l) {
+            la[l] = {&a, l, b};
+            pthread_create(&th[l], nullptr, lane_main, &la[l]);
+        }
+        for (int l = 0; l < WAVE; ++l) pthread_join(th[l], nullptr);
+    }
+    pthread_barrier_destroy(&g_bar);
+    FILE* o = fopen(argv[2], "wb");
+    if (!o) return 2;
+    fwrite(X.data(), sizeof(double), X.size(), o);
+    fwrite(U.data(), sizeof(double), U.size(), o);
+    fwrite(S.data(), sizeof(double), S.size(), o);
+    fwrite(status.data(), sizeof(int), B, o);
+    fwrite(iters.data(), sizeof(int), B, o);
+    fwrite(sqp.data(), sizeof(int), B, o);
+    fclose(o);
+    return 0;
+}
