@@ -59,6 +59,12 @@ def main():
                     help="also run B egos per GPU through the device closed loop (mpc_closed_loop, SURVEY 8(f)1) "
                          "on the config's trajectory and FSM preset, gather their check quantities to rank 0 and "
                          "report closed-loop ego-steps/s (0: skip)")
+    ap.add_argument("--plan-chunks", type=int, default=16384, metavar="B",
+                    help="offline-planner leg (SURVEY 8(f)4, libmpcplan): B chunk NLPs per GPU posed as "
+                         "optimize_full_trajectory poses them (20 m chunks, per-chunk horizon) on --plan-route; "
+                         "reported as 'plan' in chunks/s, never as 'value' (0: skip)")
+    ap.add_argument("--plan-steps", type=int, default=3, metavar="K")
+    ap.add_argument("--plan-route", default="traj3")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: a stand-in that runs the same sharded path on libmpcqp's host backend (device = -1) "
                          "with gloo, for the launcher tests; never a measurement")
@@ -192,6 +198,9 @@ def main():
 
     # closed-loop leg on every rank (its own ego shard), one gather to rank 0; after the headline timing
     cl = closed_loop(args.config, args.closed_loop, N, dev_index, world, rank, dev) if args.closed_loop else None
+    # offline-planner leg on every rank (its own chunk shard)
+    plan = plan_leg(args.plan_chunks, args.plan_steps, args.plan_route, world, rank, dev, args.cpu_seconds,
+                    not args.no_cpu) if (args.plan_chunks and gpu) else None
 
     if rank == 0:
         out = {
@@ -243,6 +252,8 @@ def main():
             out["inflight"] = inflight(args.inflight, args.steps, wb, B, N, mo, X, U, dev, head)
         if cl is not None:
             out["closed_loop"] = cl
+        if plan is not None:
+            out["plan"] = plan
         if not args.no_cpu and gpu:
             out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
             out["cpu_backend"] = cpu_backend(wb, N, mo, min(args.cpu_seconds, 5.0))
@@ -439,6 +450,160 @@ def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_ego
             "note": "restated trajectory_tracking_check verdicts applied by rank 0 to the gathered per-ego check "
                     "quantities; real-time check = each batched step's device time (the latency of every ego's "
                     "answer)"}
+
+
+def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
+    """Offline planner: B chunk NLPs per GPU (workloads.plan_batch_ref: 20 m chunks at random
+    positions of the route, each with the reference's own horizon rule, 10% final chunks), solved on the device
+    by libmpcplan, one launch per horizon (the chunks come sorted by N, so each launch sizes its LDS for its
+    own N) on one stream; `steps` timed passes over the batch after one warm-up, HIP events on that stream,
+    max over ranks.  On rank 0 also: the oracle (oracle/plan_oracle.c, OpenMP) and the restated reference
+    path (scipy SLSQP on the chunk NLP, oracle/plan_ref.py) on bounded samples of the same chunks, and the
+    GPU-vs-oracle agreement on the oracle's sample."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import mpcplan
+    import shard
+    import workloads as W
+    r = W.plan_route(route_name)
+    lo, hi = shard.shard_range(world * B, world, rank)
+    wb = W.plan_batch_ref(r, hi - lo, seed=7, offset=lo)
+    Bl = hi - lo
+    Nv = wb["N"]
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=int(Nv.max())))
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    x0, st, fin, Nd = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32), t(Nv, torch.int32)
+    groups = []
+    for n in np.unique(Nv):
+        i0, i1 = np.searchsorted(Nv, n), np.searchsorted(Nv, n, side="right")
+        groups.append((int(n), int(i0), int(i1), torch.empty((i1 - i0, n + 1, 5), dtype=torch.float64, device=dev),
+                       torch.empty((i1 - i0, n, 2), dtype=torch.float64, device=dev),
+                       torch.empty((i1 - i0, n), dtype=torch.float64, device=dev)))
+    o = [torch.empty(Bl, dtype=torch.int32, device=dev) for _ in range(3)]
+    stream = torch.cuda.current_stream(dev)
+    # the horizon groups run concurrently on side streams (a launch's time is set by its slowest chunk,
+    # so serialised launches would add their tails), the largest horizons first
+    side = [torch.cuda.Stream(dev) for _ in range(min(4, len(groups)))]
+    order = sorted(range(len(groups)), key=lambda g: -groups[g][0])
+    d8, d4 = 8, 4
+
+    def step():
+        e0 = torch.cuda.Event()
+        e0.record(stream)
+        for k, g in enumerate(order):
+            n, i0, i1, Xg, Ug, Sg = groups[g]
+            ss = side[k % len(side)]
+            if k < len(side):
+                ss.wait_event(e0)
+            pl.solve_chunks_device(i1 - i0, n, Nd.data_ptr() + d4 * i0, x0.data_ptr() + d8 * 5 * i0,
+                                   st.data_ptr() + d8 * i0, fin.data_ptr() + d4 * i0, Xg.data_ptr(), Ug.data_ptr(),
+                                   Sg.data_ptr(), o[0].data_ptr() + d4 * i0, o[1].data_ptr() + d4 * i0,
+                                   o[2].data_ptr() + d4 * i0, stream=ss.cuda_stream)
+        for ss in side:
+            e = torch.cuda.Event()
+            e.record(ss)
+            stream.wait_event(e)
+    step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(steps):
+        step()
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])
+    el = max(wall, ms.sum() / 1e3)
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    status, iters, sqp = (a.cpu().numpy() for a in o)
+    out = None
+    if rank == 0:
+        out = {"metric": "offline-planner chunk NLPs solved/s", "value": world * Bl * steps / el, "unit": "chunks/s",
+               "ms_per_step": el * 1e3 / steps, "chunks_per_gpu": Bl, "steps": steps, "dtype": "f64",
+               "workload": f"{route_name} (the committed trajectory{route_name[4:]}.json line, 50 then 30 km/h; "
+                           f"{r.s_total:.0f} m), 20 m chunks as optimize_full_trajectory poses them "
+                           f"(trajectory_planning.py:491-515), 10% final chunks, seed 7 (workloads.plan_batch_ref)",
+               "horizons": {int(n): int(c) for n, c in zip(*np.unique(Nv, return_counts=True))},
+               "status_counts_rank0": np.bincount(status, minlength=5).tolist(),
+               "status_names": [mpcplan.STATUS_NAMES[i] for i in range(5)],
+               "sqp_mean": float(sqp.mean()), "qp_ipm_iters_mean": float(iters.mean()),
+               "launches_per_step": len(groups), "streams": len(side),
+               "note": "HIP events on the timing stream, which joins the side streams that run one launch per "
+                       "horizon; inputs resident in HBM"}
+        if with_cpu:
+            out["cpu_baseline"], out["parity_sample"] = plan_cpu_baseline(r, wb, cpu_s, status, groups)
+            out["cpu_reference"] = plan_cpu_reference(r, wb)
+    pl.close()
+    return out
+
+
+def plan_cpu_baseline(route, wb, budget_s, status, groups):
+    """The planner oracle (oracle/plan_oracle.c, the same SQP / QP algorithm) with OpenMP on the host CPUs,
+    on a bounded sample of the same chunks; and the GPU's agreement with it on that sample."""
+    import numpy as np
+    import plan_oracle as PO
+    hw = host_cores()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hw["affinity_cpus"]
+    po = PO.PlanOracle(route)
+    B = wb["x0"].shape[0]
+    n = min(B, 256)
+    idx = np.linspace(0, B - 1, n).astype(int)           # spread over the horizons
+    p = PO.default_params(N=int(wb["N"].max()))
+    args = (wb["x0"][idx], wb["s_target"][idx], wb["is_final"][idx])
+    ref = po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads)
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads)
+        done += n
+    dt = time.perf_counter() - t0
+    # GPU vs oracle on the sample: X of chunks both call converged (status 0 / 4)
+    dmax, agree, both = 0.0, 0, 0
+    for j, i in enumerate(idx):
+        for nn, i0, i1, Xg, _, _ in groups:
+            if i0 <= i < i1:
+                xg = Xg[i - i0].cpu().numpy()
+                break
+        agree += int(status[i] == ref["status"][j])
+        if status[i] in (0, 4) and ref["status"][j] in (0, 4):
+            both += 1
+            dmax = max(dmax, float(np.abs(xg - ref["X"][j][:nn + 1]).max()))
+    base = {"value": done / dt, "unit": "chunks/s", "cores": threads, "kind": "port", "host": hw,
+            "sample": f"{n} chunks spread over the batch (all horizons), solved repeatedly for {dt:.1f} s by the "
+                      f"planner oracle (oracle/plan_oracle.c, the same SQP and QP algorithm) with OpenMP, "
+                      f"{threads} threads"}
+    par = {"chunks": n, "status_agreement": agree / n, "both_converged": both, "max_abs_dX_both_converged": dmax}
+    return base, par
+
+
+def plan_cpu_reference(route, wb):
+    """The reference's own chunk solve (scipy SLSQP, finite-difference gradients, maxiter 500 / ftol 1e-4,
+    trajectory_planning.py:381-387) on the restated NLP functions (oracle/plan_ref.py), one chunk at a time
+    per process over a sample of the same chunks (one pass: one chunk per process)."""
+    import numpy as np
+    from concurrent.futures import ProcessPoolExecutor
+    procs = min(16, host_cores()["affinity_cpus"])
+    B = wb["x0"].shape[0]
+    idx = np.linspace(0, B - 1, min(B, procs)).astype(int)
+    jobs = [(route.name, wb["x0"][i], float(wb["s_target"][i]), bool(wb["is_final"][i]), int(wb["N"][i]))
+            for i in idx]
+    import multiprocessing as mp
+    import plan_ref as PR
+    # one chunk per process (a chunk takes tens of seconds on this path, so the sample is one pass)
+    t0 = time.perf_counter()
+    with ProcessPoolExecutor(procs, mp_context=mp.get_context("spawn")) as ex:
+        done = sum(ex.map(PR.slsqp_job, jobs))
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "chunks/s", "cores": procs, "kind": "port",
+            "sample": f"{done} SLSQP chunk solves (finite-difference gradients, maxiter 500, ftol 1e-4: the "
+                      f"reference's minimize call) of {len(idx)} chunks of the same batch in {dt:.1f} s, "
+                      f"{procs} processes (oracle/plan_ref.py)"}
 
 
 def cpu_baseline(wb, N, mo, budget_s):

@@ -247,3 +247,12 @@ class Chunk:
         return np.diag(H), g, A, b, C, -c0
 
 
+
+
+def slsqp_job(job):
+    """One chunk through the reference's solve (for bench.py's cpu_reference leg, a process-pool worker):
+    job = (route name of workloads.plan_route, x0, s_target, is_final, N)."""
+    import workloads as W
+    name, x0, st, fin, N = job
+    Chunk(W.plan_route(name), N, 0.3, x0, st, fin).slsqp()
+    return 1

@@ -114,17 +114,22 @@ int plan_create(const double* s, int M, const double* cx, const double* cy, cons
     c->device = device;
     c->p = *p;
     c->lds_max = (size_t)lds;
+    // route arrays (s | cx | cy | vmax) followed by the search grid (ints), one allocation
+    const int T = std::max(64, std::min(1 << 18, 4 * M));
     const size_t n = (size_t)M + 8 * (size_t)(M - 1) + M;
-    if (hipMalloc(&c->d_route, n * sizeof(double)) != hipSuccess) {
+    const size_t nb = n * sizeof(double) + sizeof(int) * (size_t)T;
+    if (hipMalloc(&c->d_route, nb) != hipSuccess) {
         delete c;
         return fail(PLAN_E_ALLOC, "route allocation failed");
     }
-    std::vector<double> h(n);
+    std::vector<double> h(n + (T + 1) / 2);
     std::memcpy(h.data(), s, sizeof(double) * M);
     std::memcpy(h.data() + M, cx, sizeof(double) * 4 * (M - 1));
     std::memcpy(h.data() + M + 4 * (M - 1), cy, sizeof(double) * 4 * (M - 1));
     std::memcpy(h.data() + M + 8 * (M - 1), vmax, sizeof(double) * M);
-    if (hipMemcpy(c->d_route, h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    double ginv = 0.0;
+    route_grid(s, M, T, (int*)(h.data() + n), &ginv);
+    if (hipMemcpy(c->d_route, h.data(), nb, hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(c->d_route);
         delete c;
         return fail(PLAN_E_DEVICE, "route upload failed");
@@ -133,6 +138,9 @@ int plan_create(const double* s, int M, const double* cx, const double* cy, cons
     c->R.cx = c->d_route + M;
     c->R.cy = c->d_route + M + 4 * (M - 1);
     c->R.vmax = c->d_route + M + 8 * (M - 1);
+    c->R.grid = (const int*)(c->d_route + n);
+    c->R.T = T;
+    c->R.ginv = ginv;
     c->R.M = M;
     c->R.s_total = s[M - 1];
     *out = c;

@@ -13,6 +13,10 @@
 #endif
 typedef PLAN_LDS_AS double ldsd;
 
+#ifdef PLAN_PROF
+__device__ unsigned long long g_plan_prof[16];
+#endif
+
 namespace {
 
 constexpr int WAVE = 64;
@@ -40,7 +44,25 @@ struct DevRoute {
     const double *s, *cx, *cy, *vmax;
     int M;
     double s_total;
+    // uniform grid over [s[0], s[M-1]]: grid[j] = first i with s[i] >= s[0] + j / ginv (route_grid), so a
+    // search starts at most a cell's worth of way-points before its answer (one load instead of a binary
+    // search's ~log2 M dependent loads from HBM)
+    const int* grid;
+    int T;
+    double ginv;
 };
+
+// the grid of DevRoute (host side; T cells of equal length)
+inline void route_grid(const double* s, int M, int T, int* grid, double* ginv) {
+    const double h = (s[M - 1] - s[0]) / T;
+    *ginv = 1.0 / h;
+    int i = 0;
+    for (int j = 0; j < T; ++j) {
+        const double c = s[0] + j * h;
+        while (i < M && s[i] < c) ++i;
+        grid[j] = i;
+    }
+}
 
 // LDS layout of one chunk (doubles; per-stage counts times NP = Nmax + 1).  Arrays used only by the interior
 // point alias the polish's: DSA = Y, DLA = TLAM, DS = TZ (the polish runs after the interior point is done).
@@ -87,6 +109,9 @@ __host__ __device__ Layout make_layout(int Nmax) {
     y.oACT = o; o += np;             // active-row bit masks (11 bits), stored as doubles
     y.oTACT = o; o += np;
     y.oSC = o; o += 16;              // scalars shared by the wave
+#ifdef PLAN_PROF
+    o += 16;                         // phase counters of the diagnostic build
+#endif
     y.oY = y.oDSA;
     y.oTLAM = y.oDLA;
     y.oTZ = y.oDS;
@@ -127,29 +152,39 @@ __device__ inline int wsumi(int v) {
 // ------------------------------------------------------------------------------------------------------
 // route: k_ref_fun (:445-459) and v_max_fun (:470-473)
 // ------------------------------------------------------------------------------------------------------
-__device__ int lower_bound_d(const double* x, int n, double v) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        if (x[m] < v) lo = m + 1; else hi = m;
-    }
-    return lo;
+__device__ inline int imin(int a, int b) { return a < b ? a : b; }
+
+// first i with x[i] >= v (std::lower_bound over R.s; NaN -> 0), from the grid cell of v
+__device__ int lower_bound_g(const DevRoute& R, double v) {
+    const double* x = R.s;
+    int j;
+    if (!(v > x[0])) return 0;
+    if (!(v < x[R.M - 1])) j = R.T - 1;
+    else j = imin(R.T - 1, (int)((v - x[0]) * R.ginv));
+    int i = R.grid[j];
+    while (i > 0 && x[i - 1] >= v) --i;      // the cell index may round up past v
+    while (i < R.M && x[i] < v) ++i;
+    return i;
 }
 
-__device__ int upper_bound_d(const double* x, int n, double v) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int m = (lo + hi) >> 1;
-        if (x[m] <= v) lo = m + 1; else hi = m;
-    }
-    return lo;
+// first i with x[i] > v (std::upper_bound over R.s; NaN -> 0), from the grid cell of v
+__device__ int upper_bound_g(const DevRoute& R, double v) {
+    const double* x = R.s;
+    int j;
+    if (!(v >= x[0])) return 0;
+    if (!(v < x[R.M - 1])) j = R.T - 1;
+    else j = imin(R.T - 1, (int)((v - x[0]) * R.ginv));
+    int i = R.grid[j];
+    while (i > 0 && x[i - 1] > v) --i;
+    while (i < R.M && x[i] <= v) ++i;
+    return i;
 }
 
 // kappa(s) with d/ds and d2/ds2 (k2 may be null): s_to_t linear (searchsorted left, clipped to [1, M-1]),
 // spline piece floor(t) clipped to [0, M-2]
 __device__ double route_kappa(const DevRoute& R, double s, double* k1, double* k2) {
     const int M = R.M;
-    int i = lower_bound_d(R.s, M, s);
+    int i = lower_bound_g(R, s);
     i = i < 1 ? 1 : (i > M - 1 ? M - 1 : i);
     const double slope = 1.0 / (R.s[i] - R.s[i - 1]);
     const double t = slope * (s - R.s[i - 1]) + (double)(i - 1);
@@ -183,7 +218,7 @@ __device__ double route_kappa(const DevRoute& R, double s, double* k1, double* k
 }
 
 __device__ double route_vmax(const DevRoute& R, double s) {
-    const int i = upper_bound_d(R.s, R.M, s);
+    const int i = upper_bound_g(R, s);
     return R.vmax[i > 0 ? i - 1 : 0];
 }
 
@@ -398,29 +433,28 @@ struct Ctx {
     double x0[5], st, den;
     double delta;       // uniform
     double xi0[5], e[2], nu[2];
-#ifdef PLAN_PROF
-    mutable unsigned long long pt, pacc[PH_COUNT];
-    mutable int pc;
-#endif
 };
 
 // phase-time instrumentation of the diagnostic build (-DPLAN_PROF, libmpcplan_prof.so, tools/plan_phase.py):
-// the wave's time between phase switches (s_memtime), summed per phase over the chunks of a launch
+// each scope adds its own elapsed s_memtime ticks (inclusive of the phases nested in it) to an LDS counter
+// (lane 0), summed into g_plan_prof at the end of the chunk
 #ifdef PLAN_PROF
-__device__ unsigned long long g_plan_prof[16];
-__device__ inline int ph(const Ctx& X, int p) {
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    X.pacc[X.pc] += t - X.pt;
-    X.pt = t;
-    const int o = X.pc;
-    X.pc = p;
-    return o;
-}
 struct PhScope {
-    const Ctx& X;
-    int o;
-    __device__ PhScope(const Ctx& x, int p) : X(x), o(ph(x, p)) {}
-    __device__ ~PhScope() { ph(X, o); }
+    ldsd* L;
+    int off, ln;
+    unsigned long long t0;
+    __device__ PhScope(const Ctx& X, int p) : L(X.L), off(X.Y.oSC + 16 + p), ln(X.ln), t0(__builtin_amdgcn_s_memtime()) {}
+    __device__ ~PhScope() {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        if (ln == 0) {
+            PLAN_LDS_AS unsigned long long* q = (PLAN_LDS_AS unsigned long long*)(L + off);
+#ifdef PLAN_PROF_COUNT
+            *q += 1;                  // host emulation: entries per phase
+#else
+            *q += t - t0;
+#endif
+        }
+    }
 };
 #define PHASE(p) PhScope ph_scope_(X, p)
 #else
@@ -1452,6 +1486,8 @@ __device__ double cost_dir(const Ctx& X) {
     return wsum(v);
 }
 
+__device__ inline ldsd* lds_p(const Ctx& X) { return X.L; }
+
 struct KArgs {
     DevRoute R;
     plan_params P;
@@ -1482,9 +1518,10 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
     X.nu[0] = X.nu[1] = 0.0;
     X.delta = 0.0;
 #ifdef PLAN_PROF
-    for (int i = 0; i < PH_COUNT; ++i) X.pacc[i] = 0;
-    X.pc = PH_OTHER;
-    X.pt = __builtin_amdgcn_s_memtime();
+    if (X.ln == 0)
+        for (int i = 0; i < 16; ++i) *(PLAN_LDS_AS unsigned long long*)(lds_p(X) + X.Y.oSC + 16 + i) = 0ull;
+    sync();
+    const unsigned long long t_total0 = __builtin_amdgcn_s_memtime();
 #endif
     ldsd* L = X.L;
     const Layout& Y = X.Y;
@@ -1622,9 +1659,10 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         if (a.sqp) a.sqp[b] = nq;
     }
 #ifdef PLAN_PROF
-    ph(X, PH_OTHER);
     if (X.ln == 0) {
-        for (int i = 0; i < PH_COUNT; ++i) atomicAdd(&g_plan_prof[i], X.pacc[i]);
+        *(PLAN_LDS_AS unsigned long long*)(lds_p(X) + X.Y.oSC + 16 + PH_OTHER) = __builtin_amdgcn_s_memtime() - t_total0;
+        for (int i = 0; i < PH_COUNT; ++i)
+            atomicAdd(&g_plan_prof[i], *(PLAN_LDS_AS unsigned long long*)(lds_p(X) + X.Y.oSC + 16 + i));
         atomicAdd(&g_plan_prof[15], 1ull);
     }
 #endif

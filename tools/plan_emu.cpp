@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -103,6 +104,11 @@ int main(int argc, char** argv) {
     a.R.vmax = vm.data();
     a.R.M = M;
     a.R.s_total = s[M - 1];
+    const int T = std::max(64, std::min(1 << 18, 4 * M));
+    std::vector<int> grid(T);
+    route_grid(s.data(), M, T, grid.data(), &a.R.ginv);
+    a.R.grid = grid.data();
+    a.R.T = T;
     a.P = P;
     a.B = B;
     a.Nmax = Nmax;

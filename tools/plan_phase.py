@@ -1,6 +1,7 @@
 """Planner phase profile: runs B chunks through the diagnostic build libmpcplan_prof.so (-DPLAN_PROF) and
-prints the share of wave time per kernel phase (s_memtime ticks summed over chunks).
-usage: python tools/plan_phase.py N B [route] [final_frac]"""
+prints the wave time per kernel phase (s_memtime ticks summed over chunks; each phase inclusive of the phases
+nested in it: factor and solve run inside ipm_rows / eqp_rows, rollout inside both), as a share of the total.
+usage: python tools/plan_phase.py N B1,B2,... [route] [final_frac]"""
 import ctypes as C
 import os
 import sys
@@ -15,29 +16,31 @@ import mpcplan
 mpcplan.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcplan_prof.so")
 import workloads as W
 
-PHASES = ["other", "build_qp", "stage_hess", "factor(lane0)", "solve", "ipm_rows", "eqp_rows", "multipliers",
+PHASES = ["TOTAL", "build_qp", "stage_hess", "factor(lane0)", "solve", "ipm_rows", "eqp_rows", "multipliers",
           "line_search", "rollout"]
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+Bs = sys.argv[2] if len(sys.argv) > 2 else "64,4096"
 route = sys.argv[3] if len(sys.argv) > 3 else "traj1"
 ff = float(sys.argv[4]) if len(sys.argv) > 4 else 0.25
 L = mpcplan.lib()
 L.plan_debug_prof.restype = C.c_int
 L.plan_debug_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 r = W.plan_route(route)
-wb = W.plan_batch(r, N, B, seed=N, final_frac=ff)
-pl = mpcplan.Planner(r, mpcplan.default_params(N=N))
-buf = (C.c_ulonglong * 16)()
-L.plan_debug_prof(buf, 1)
-t0 = time.perf_counter()
-g = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
-wall = time.perf_counter() - t0
-L.plan_debug_prof(buf, 0)
-v = np.array(buf[:len(PHASES)], dtype=np.float64)
-tot = v.sum()
-print(f"N={N} B={B} {route}: wall {wall * 1e3:.1f} ms, chunks counted {buf[15]}, sqp mean {g['sqp'].mean():.2f}, "
-      f"ipm iters mean {g['iters'].mean():.1f}, status {np.bincount(g['status'], minlength=5).tolist()}")
-print(f"ticks per chunk {tot / max(1, buf[15]):.3e}")
-for n, x in zip(PHASES, v):
-    print(f"  {n:14s} {x / tot * 100:6.2f}%   {x / max(1, buf[15]):.3e} ticks/chunk")
+for B in [int(x) for x in Bs.split(",")]:
+    wb = W.plan_batch(r, N, B, seed=N, final_frac=ff)
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=N))
+    buf = (C.c_ulonglong * 16)()
+    print(f"B={B}: reset rc {L.plan_debug_prof(buf, 1)}", flush=True)
+    t0 = time.perf_counter()
+    g = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    wall = time.perf_counter() - t0
+    L.plan_debug_prof(buf, 0)
+    v = np.array(buf[:len(PHASES)], dtype=np.float64)
+    tot = v[0]
+    print(f"N={N} B={B} {route}: wall {wall * 1e3:.1f} ms, chunks counted {buf[15]}, sqp mean {g['sqp'].mean():.2f}, "
+          f"ipm iters mean {g['iters'].mean():.1f}, status {np.bincount(g['status'], minlength=5).tolist()}")
+    print(f"ticks per chunk {tot / max(1, buf[15]):.3e}")
+    for n, x in zip(PHASES, v):
+        print(f"  {n:14s} {x / max(tot, 1) * 100:6.2f}%   {x / max(1, buf[15]):.3e} ticks/chunk", flush=True)
+    pl.close()
