@@ -196,6 +196,7 @@ def main():
         except Exception:
             traffic = None
 
+    executed = executed_work(args.config)
     # closed-loop leg on every rank (its own ego shard), one gather to rank 0; after the headline timing
     cl = closed_loop(args.config, args.closed_loop, N, dev_index, world, rank, dev) if args.closed_loop else None
     # offline-planner leg on every rank (its own chunk shard)
@@ -239,7 +240,9 @@ def main():
                          "note": "HIP events on the launch stream; a step is the path's launch pair: crossover "
                                  "kernel + interior-point kernel on the deferred instances (DESIGN.md 3); traffic = "
                                  "PMC HBM bytes per step (profiles/pmc_hbm_bytes.json)",
-                         "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9},
+                         "hbm_algorithmic_GBs": nbytes / avg_launch_s / 1e9,
+                         "executed_frac": executed.get("executed_frac"), "valu_busy": executed.get("valu_busy"),
+                         "executed": executed},
         }
         if not gpu:
             out["device"] = "cpu-standin"
@@ -450,6 +453,32 @@ def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_ego
             "note": "restated trajectory_tracking_check verdicts applied by rank 0 to the gathered per-ego check "
                     "quantities; real-time check = each batched step's device time (the latency of every ego's "
                     "answer)"}
+
+
+def executed_work(config):
+    """Executed FP64 work of this config's dominant kernel from the last PMC pass over it (rocprofv3 --pmc
+    SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64, SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES in their own
+    run: tools/gpu_f64_pmc.sh, summarised by tools/pmc_f64.py into profiles/r04_pmc_f64_<config>.csv).
+    executed_frac = (2 FMA + MUL + ADD + TRANS) x 64 lanes / kernel time / 78.6 TF: an upper bound, since the
+    recursions issue under narrowed exec masks; valu_busy = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES."""
+    import csv
+    path = os.path.join(ROOT, "profiles", f"r04_pmc_f64_{config}.csv")
+    if not os.path.exists(path):
+        return {}
+    rows = list(csv.DictReader(open(path)))
+    if not rows:
+        return {}
+    top = max(rows, key=lambda r: float(r.get("avg_duration_s") or 0.0))
+    f = lambda r, k: float(r[k]) if r.get(k) not in (None, "") else None
+    return {"executed_frac": f(top, "executed_frac_upper"), "valu_busy": f(top, "valu_busy"),
+            "kernel": top["kernel"], "source": f"profiles/r04_pmc_f64_{config}.csv",
+            "per_kernel": {r["kernel"]: {"executed_TFLOPs_upper": f(r, "executed_TFLOPs_upper"),
+                                         "executed_frac_upper": f(r, "executed_frac_upper"),
+                                         "valu_busy": f(r, "valu_busy"), "fp64_insts": f(r, "fp64_insts"),
+                                         "avg_duration_s": f(r, "avg_duration_s")} for r in rows},
+            "basis": "FP64 VALU instruction counts x 64 lanes / the kernel's average duration (upper bound: "
+                     "the Riccati recursions issue under exec masks of 5-10 lanes); valu_busy = "
+                     "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES"}
 
 
 def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):

@@ -184,6 +184,11 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
     a.B = B;
     a.Nmax = Nmax;
     a.Nfixed = c->p.N;
+    // PLAN_DBG (diagnostics only): repeats a phase for A/B timing, the results do not change.  Bits: 1 each
+    // interior-point factorisation, 2 each solve, 4 the interior point's gradient/row loop, 8 its direction
+    // loop, 16 build_qp, 32 multipliers, 64 each line-search merit evaluation
+    const char* dbg = std::getenv("PLAN_DBG");
+    a.dbg = dbg ? std::atoi(dbg) : 0;
     a.N = N;
     a.x0 = x0;
     a.st = s_target;

@@ -69,7 +69,7 @@ inline void route_grid(const double* s, int M, int T, int* grid, double* ginv) {
 struct Layout {
     int NP;
     int oA, oB, oC, oH, oHT, oGQ, oG, oK, oL, oEZ, oZ, oS, oLAM, oGL, oDZ, oDSA, oDLA, oDS, oDL, oMY, oMLAT, oZB,
-        oZ2, oDZV, oPI, oVLIM, oVL, oACT, oTACT, oSC;
+        oZ2, oDZV, oPI, oVLIM, oVL, oACT, oTACT, oSC, oWK;
     int oY, oTLAM, oTZ;
     int total;
 };
@@ -112,6 +112,7 @@ __host__ __device__ Layout make_layout(int Nmax) {
 #ifdef PLAN_PROF
     o += 16;                         // phase counters of the diagnostic build
 #endif
+    y.oWK = o; o += 96;              // factorisation work area: P (25), M (64)
     y.oY = y.oDSA;
     y.oTLAM = y.oDLA;
     y.oTZ = y.oDS;
@@ -317,30 +318,22 @@ __device__ void defect(const DevRoute& R, const plan_params& P, const double xa[
     for (int i = 0; i < 5; ++i) def[i] = xb[i] - (xa[i] + P.defect_sign * (h / 6.0) * (fa[i] + 4.0 * fm[i] + fb[i]));
 }
 
-// the rows of stage k (kinds in order) — the structure of build_qp in the oracle
-__device__ int stage_rows(int k, int N, int fin, int kinds[NR]) {
-    int n = 0;
-    if (!(fin && k == N)) {
-        kinds[n++] = ROW_VMIN;
-        kinds[n++] = ROW_VMAX;
-        if (k > 0) {
-            kinds[n++] = ROW_LATP;
-            kinds[n++] = ROW_LATM;
-        }
-    }
-    if (k > 0) {
-        kinds[n++] = ROW_KMIN;
-        kinds[n++] = ROW_KMAX;
-    }
-    if (k < N) {
-        kinds[n++] = ROW_U1MIN;
-        kinds[n++] = ROW_U1MAX;
-        kinds[n++] = ROW_U2MIN;
-        kinds[n++] = ROW_U2MAX;
-        kinds[n++] = ROW_S;
-    }
-    if (k == N && !fin) kinds[n++] = ROW_STERM;
-    return n;
+// the rows of stage k, in order: [v_min, v_max, (k > 0) lateral +, lateral -] unless the final chunk's last
+// stage; (k > 0) curvature min, max; (k < N) u1 min, max, u2 min, max, slack; the intermediate chunk's
+// terminal row at k = N.  Counted and indexed arithmetically (no per-lane array, which would live in
+// scratch memory).
+__device__ inline int stage_nrows(int k, int N, int fin) {
+    return ((fin && k == N) ? 0 : (k > 0 ? 4 : 2)) + (k > 0 ? 2 : 0) + (k < N ? 5 : 0) + ((k == N && !fin) ? 1 : 0);
+}
+__device__ inline int row_kind(int k, int N, int fin, int j) {
+    const int n0 = (fin && k == N) ? 0 : (k > 0 ? 4 : 2);
+    if (j < n0) return j;                                   // ROW_VMIN, ROW_VMAX, ROW_LATP, ROW_LATM
+    j -= n0;
+    const int n1 = k > 0 ? 2 : 0;
+    if (j < n1) return ROW_KMIN + j;
+    j -= n1;
+    if (k < N) return ROW_U1MIN + j;                        // ROW_U1MIN .. ROW_S
+    return ROW_STERM;
 }
 
 // coefficients of a row over (x_k, w_k), at the SQP iterate's (k, v) of stage k
@@ -391,28 +384,32 @@ __device__ bool solve5(double M[25], double R[5 * NC]) {
     return true;
 }
 
+// L L' = H (3 x 3) with the diagonal of L stored inverted (L[0] = 1/l00, L[2] = 1/l11, L[5] = 1/l22), so
+// the solves multiply instead of divide: 3 divisions per factorisation instead of 6 per solve, which sit on
+// the solves' dependent chains (oracle/plan_oracle.c uses the same form and rounding)
 __device__ bool chol3(const double H[3][3], double L[6]) {
     if (!(H[0][0] > 0.0)) return false;
-    L[0] = sqrt(H[0][0]);
-    L[1] = H[1][0] / L[0];
+    L[0] = 1.0 / sqrt(H[0][0]);
+    L[1] = H[1][0] * L[0];
     const double d1 = H[1][1] - L[1] * L[1];
     if (!(d1 > 0.0)) return false;
-    L[2] = sqrt(d1);
-    L[3] = H[2][0] / L[0];
-    L[4] = (H[2][1] - L[3] * L[1]) / L[2];
+    L[2] = 1.0 / sqrt(d1);
+    L[3] = H[2][0] * L[0];
+    L[4] = (H[2][1] - L[3] * L[1]) * L[2];
     const double d2 = H[2][2] - L[3] * L[3] - L[4] * L[4];
     if (!(d2 > 0.0)) return false;
-    L[5] = sqrt(d2);
+    L[5] = 1.0 / sqrt(d2);
     return true;
 }
 
+// b <- (L L')^-1 b
 __device__ inline void chol3_solve(const double L[6], double b[3]) {
-    const double y0 = b[0] / L[0];
-    const double y1 = (b[1] - L[1] * y0) / L[2];
-    const double y2 = (b[2] - L[3] * y0 - L[4] * y1) / L[5];
-    b[2] = y2 / L[5];
-    b[1] = (y1 - L[4] * b[2]) / L[2];
-    b[0] = (y0 - L[1] * b[1] - L[3] * b[2]) / L[0];
+    const double y0 = b[0] * L[0];
+    const double y1 = (b[1] - L[1] * y0) * L[2];
+    const double y2 = (b[2] - L[3] * y0 - L[4] * y1) * L[5];
+    b[2] = y2 * L[5];
+    b[1] = (y1 - L[4] * b[2]) * L[2];
+    b[0] = (y0 - L[1] * b[1] - L[3] * b[2]) * L[0];
 }
 
 __host__ __device__ constexpr int hx(int i, int j) {   // packed index of the symmetric 8x8 (i <= j)
@@ -430,6 +427,7 @@ struct Ctx {
     ldsd* L;            // the chunk's LDS block (explicit address space: ds_read / ds_write, never flat)
     int ln;             // lane
     int N, fin;
+    int dbg;            // A/B timing switches (PLAN_DBG, plan.hip): repeat a phase, results unchanged
     double x0[5], st, den;
     double delta;       // uniform
     double xi0[5], e[2], nu[2];
@@ -704,12 +702,11 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
                 }
             }
         }
-        int kinds[NR];
-        const int nr = stage_rows(k, N, X.fin, kinds);
+        const int nr = stage_nrows(k, N, X.fin);
         const double kk = x[3], v = x[4];
         for (int j = 0; j < nr; ++j) {
             double gv = 0.0;
-            switch (kinds[j]) {
+            switch (row_kind(k, X.N, X.fin, j)) {
                 case ROW_VMIN: gv = v + sl - P.v_min; break;
                 case ROW_VMAX: gv = (frozen ? L[Y.oVLIM + k] : route_vmax(X.R, x[0])) - (v + sl); break;
                 case ROW_LATP: gv = P.a_max - kk * v * v; break;
@@ -756,13 +753,12 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
 #pragma unroll
         for (int i = 0; i < NZ; ++i)
             if (i < nv) H[hx(i, i)] += X.delta;
-        int kinds[NR];
-        const int nr = stage_rows(k, N, X.fin, kinds);
+        const int nr = stage_nrows(k, N, X.fin);
         for (int j = 0; j < nr; ++j) {
             const double w = mode == 0 ? L[Y.oLAM + NR * k + j] / L[Y.oS + NR * k + j] : (act_bit(X, Y.oTACT, k, j) ? RHO : 0.0);
             if (w == 0.0) continue;
             double a[NZ];
-            coef_of(X, k, kinds[j], a);
+            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
 #pragma unroll
             for (int u = 0; u < NZ; ++u)
 #pragma unroll
@@ -773,11 +769,25 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
     }
 }
 
-// LQ solve (lane 0) with zero initial state and homogeneous dynamics: stage linear terms at ogl -> odz
+// v of lane src in every lane (v_readlane into scalar registers: no LDS round trip)
+#ifndef PLAN_HOST_EMU
+__device__ inline double bcast(double v, int src) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+    return __hiloint2double(hi, lo);
+}
+#endif
+
+// LQ solve over the wave with zero initial state and homogeneous dynamics: stage linear terms at ogl ->
+// odz (lane 0 stores; the caller syncs before reading odz).  Per stage the 3-vectors (control rhs, Cholesky
+// solve, feedback) are computed by every lane alike, and the 5-vectors of the recursions (co-state p
+// backwards, state x forwards) one entry per lane on lanes 0..4 and broadcast by readlane.  Every entry
+// is formed by the same operations in the same order as on one lane, so the result is the same.
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     const int N = X.N;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
+    const int me = X.ln < 5 ? X.ln : 0;
     double p[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = L[ogl + NZ * N + i];
@@ -795,23 +805,21 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         h[2] = L[ogl + NZ * k + 7];
         double t[3] = {-h[0], -h[1], -h[2]};
         chol3_solve(Lc, t);
+        if (X.ln == 0)
 #pragma unroll
-        for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = t[i];
+            for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = t[i];
         if (k > 0) {
-            double pn[5];
+            double v = L[ogl + NZ * k + me];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                double v = L[ogl + NZ * k + i];
+            for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + me] * p[l];
 #pragma unroll
-                for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + i] * p[l];
+            for (int l = 0; l < 3; ++l) v += L[Y.oK + 15 * k + 5 * l + me] * h[l];
 #pragma unroll
-                for (int l = 0; l < 3; ++l) v += L[Y.oK + 15 * k + 5 * l + i] * h[l];
-                pn[i] = v;
-            }
-#pragma unroll
-            for (int i = 0; i < 5; ++i) p[i] = pn[i];
+            for (int i = 0; i < 5; ++i) p[i] = bcast(v, i);
         }
     }
+    // the forward pass reads the control parts just stored
+    sync();
     double x[5] = {0, 0, 0, 0, 0};
     for (int k = 0; k < N; ++k) {
         double w[3];
@@ -822,133 +830,133 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
             for (int l = 0; l < 5; ++l) v += L[Y.oK + 15 * k + 5 * i + l] * x[l];
             w[i] = v;
         }
+        double v = 0.0;
 #pragma unroll
-        for (int i = 0; i < 5; ++i) L[odz + NZ * k + i] = x[i];
+        for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * me + l] * x[l];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = w[i];
+        for (int l = 0; l < 2; ++l) v += L[Y.oB + 10 * k + 2 * me + l] * w[l];
+        // stage k overwritten after every lane has read its control part (the broadcast orders that)
         double xn[5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            double v = 0.0;
+        for (int i = 0; i < 5; ++i) xn[i] = bcast(v, i);
+        if (X.ln == 0) {
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * i + l] * x[l];
+            for (int i = 0; i < 5; ++i) L[odz + NZ * k + i] = x[i];
 #pragma unroll
-            for (int l = 0; l < 2; ++l) v += L[Y.oB + 10 * k + 2 * i + l] * w[l];
-            xn[i] = v;
+            for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = w[i];
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) x[i] = xn[i];
     }
+    if (X.ln == 0) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) L[odz + NZ * N + i] = x[i];
+        for (int i = 0; i < 5; ++i) L[odz + NZ * N + i] = x[i];
 #pragma unroll
-    for (int i = 5; i < NZ; ++i) L[odz + NZ * N + i] = 0.0;
+        for (int i = 5; i < NZ; ++i) L[odz + NZ * N + i] = 0.0;
+    }
 }
 
-// Riccati factorisation (lane 0) of the HT stage Hessians; false when a control pivot is not positive
-__device__ bool factor_serial(const Ctx& X) {
-    const int N = X.N;
+// [A_k | B_k] (5 x 7: the state and the two control columns; the slack enters no dynamics) at (l, j)
+__device__ inline double ab_at(const Ctx& X, int k, int l, int j) {
+    return j < 5 ? X.L[X.Y.oA + 25 * k + 5 * l + j] : X.L[X.Y.oB + 10 * k + 2 * l + (j - 5)];
+}
+
+// Riccati factorisation of the HT stage Hessians over the wave (uniform result: false when a control
+// pivot is not positive, or the final chunk's terminal system is singular).  Per stage, backwards:
+//   M = HT + [A B 0]' P [A B 0]  (xx, wx, ww)       49 lanes, one entry each (the column of P [A B] it
+//                                                   needs formed in the lane)
+//   Mww = L L' (every lane), K = -Mww^-1 Mwx        5 lanes store one gain column each
+//   P <- sym(Mxx + Mwx' K)                          25 lanes (forming the two gain columns they need)
+// two wave barriers per stage; every entry is formed by the same operations in the same order as the
+// recursion on one lane (round-4 first cut), so the rounding is the same, and the chain per stage is ~50
+// dependent FP64 operations instead of ~1100 issued on one lane.
+__device__ bool factor_par(const Ctx& X) {
+    const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
-    double P[25];
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) P[5 * i + j] = L[Y.oHT + NH * N + hidx(i, j)];
+    ldsd* P = L + Y.oWK;
+    ldsd* M = P + 25;
+    if (ln < 25) P[ln] = L[Y.oHT + NH * N + hidx(ln / 5, ln % 5)];
+    sync();
     for (int k = N - 1; k >= 0; --k) {
-        double A[25], Bm[10], PA[25], PB[10], Hww[3][3], Hwx[15], Lc[6], H[NH];
+        if (ln < 49) {
+            int u, w;
+            if (ln < 25) { u = ln / 5; w = ln % 5; }
+            else if (ln < 40) { u = 5 + (ln - 25) / 5; w = (ln - 25) % 5; }
+            else { u = 5 + (ln - 40) / 3; w = 5 + (ln - 40) % 3; }
+            double m = L[Y.oHT + NH * k + hidx(u, w)];
+            if (u < 7 && w < 7) {
+                double pab[5];                      // column w of P [A | B], formed in this lane
 #pragma unroll
-        for (int i = 0; i < NH; ++i) H[i] = L[Y.oHT + NH * k + i];
+                for (int i = 0; i < 5; ++i) {
+                    double v = 0.0;
 #pragma unroll
-        for (int i = 0; i < 25; ++i) A[i] = L[Y.oA + 25 * k + i];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) Bm[i] = L[Y.oB + 10 * k + i];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                double v = 0.0;
-#pragma unroll
-                for (int l = 0; l < 5; ++l) v += P[5 * i + l] * A[5 * l + j];
-                PA[5 * i + j] = v;
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                double v = 0.0;
-#pragma unroll
-                for (int l = 0; l < 5; ++l) v += P[5 * i + l] * Bm[2 * l + j];
-                PB[2 * i + j] = v;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                double v = H[hidx(5 + i, 5 + j)];
-                if (i < 2 && j < 2)
-#pragma unroll
-                    for (int l = 0; l < 5; ++l) v += Bm[2 * l + i] * PB[2 * l + j];
-                Hww[i][j] = v;
-            }
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                double v = H[hidx(5 + i, j)];
-                if (i < 2)
-#pragma unroll
-                    for (int l = 0; l < 5; ++l) v += Bm[2 * l + i] * PA[5 * l + j];
-                Hwx[5 * i + j] = v;
-            }
-        }
-        if (!chol3(Hww, Lc)) return false;
-        double K[15];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            double col[3] = {-Hwx[j], -Hwx[5 + j], -Hwx[10 + j]};
-            chol3_solve(Lc, col);
-            K[j] = col[0];
-            K[5 + j] = col[1];
-            K[10 + j] = col[2];
-        }
-#pragma unroll
-        for (int i = 0; i < 15; ++i) L[Y.oK + 15 * k + i] = K[i];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) L[Y.oL + 6 * k + i] = Lc[i];
-        if (k > 0) {
-            double Pn[25];
-#pragma unroll
-            for (int i = 0; i < 5; ++i)
-#pragma unroll
-                for (int j = 0; j < 5; ++j) {
-                    double v = H[hidx(i, j)];
-#pragma unroll
-                    for (int l = 0; l < 5; ++l) v += A[5 * l + i] * PA[5 * l + j];
-#pragma unroll
-                    for (int l = 0; l < 3; ++l) v += Hwx[5 * l + i] * K[5 * l + j];
-                    Pn[5 * i + j] = v;
+                    for (int l = 0; l < 5; ++l) v += P[5 * i + l] * ab_at(X, k, l, w);
+                    pab[i] = v;
                 }
 #pragma unroll
-            for (int i = 0; i < 5; ++i)
-#pragma unroll
-                for (int j = 0; j < 5; ++j) P[5 * i + j] = 0.5 * (Pn[5 * i + j] + Pn[5 * j + i]);
+                for (int l = 0; l < 5; ++l) m += ab_at(X, k, l, u) * pab[l];
+            }
+            M[8 * u + w] = m;
         }
+        sync();
+        double Hww[3][3], Lc[6];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Hww[r][c] = M[8 * (5 + r) + 5 + c];
+        if (!chol3(Hww, Lc)) return false;
+        // gain column j = -Mww^-1 Mwx(:, j): lanes 0..4 store theirs; the P lanes form the two they need
+        auto gain = [&](int j, double col[3]) {
+            col[0] = -M[8 * 5 + j];
+            col[1] = -M[8 * 6 + j];
+            col[2] = -M[8 * 7 + j];
+            chol3_solve(Lc, col);
+        };
+        if (ln < 5) {
+            double col[3];
+            gain(ln, col);
+            L[Y.oK + 15 * k + ln] = col[0];
+            L[Y.oK + 15 * k + 5 + ln] = col[1];
+            L[Y.oK + 15 * k + 10 + ln] = col[2];
+        } else if (ln < 11) {
+            L[Y.oL + 6 * k + ln - 5] = Lc[ln - 5];
+        }
+        if (k > 0 && ln < 25) {
+            const int i = ln / 5, j = ln % 5;
+            double ki[3], kj[3];
+            gain(i, ki);
+            gain(j, kj);
+            double a = M[8 * i + j], b = M[8 * j + i];
+#pragma unroll
+            for (int l = 0; l < 3; ++l) a += M[8 * (5 + l) + i] * kj[l];
+#pragma unroll
+            for (int l = 0; l < 3; ++l) b += M[8 * (5 + l) + j] * ki[l];
+            P[ln] = 0.5 * (a + b);
+        }
+        sync();
     }
     if (X.fin) {
         for (int c = 0; c < 2; ++c) {
-            for (int k = 0; k <= N; ++k)
+            for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) L[Y.oGL + NZ * k + i] = 0.0;
-            L[Y.oGL + NZ * N + (c == 0 ? 0 : 4)] = 1.0;
+                for (int i = 0; i < NZ; ++i) L[Y.oGL + NZ * k + i] = (k == N && i == (c == 0 ? 0 : 4)) ? 1.0 : 0.0;
+            sync();
             solve_core(X, Y.oGL, Y.oDZ);
-            for (int k = 0; k <= N; ++k)
+            sync();
+            for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) L[Y.oEZ + 2 * NZ * k + NZ * c + i] = L[Y.oDZ + NZ * k + i];
+            sync();
         }
         const double e0 = L[Y.oEZ + 2 * NZ * N + 0], e1 = L[Y.oEZ + 2 * NZ * N + NZ + 0];
         const double e2 = L[Y.oEZ + 2 * NZ * N + 4], e3 = L[Y.oEZ + 2 * NZ * N + NZ + 4];
-        L[Y.oSC + SC_EM0] = e0;
-        L[Y.oSC + SC_EM1] = e1;
-        L[Y.oSC + SC_EM2] = e2;
-        L[Y.oSC + SC_EM3] = e3;
+        if (ln == 0) {
+            L[Y.oSC + SC_EM0] = e0;
+            L[Y.oSC + SC_EM1] = e1;
+            L[Y.oSC + SC_EM2] = e2;
+            L[Y.oSC + SC_EM3] = e3;
+        }
         const double det = e0 * e3 - e1 * e2;
         if (!(fabs(det) > 0.0) || !isfinite(det)) return false;
     }
@@ -960,13 +968,12 @@ __device__ bool factor_reg(Ctx& X, int mode) {
     for (;;) {
         stage_hess_par(X, mode);
         sync();
+        bool ok;
         {
             PHASE(PH_FACTOR);
-            if (X.ln == 0) X.L[X.Y.oSC + SC_FLAG] = factor_serial(X) ? 1.0 : 0.0;
+            ok = factor_par(X);
             sync();
         }
-        const bool ok = X.L[X.Y.oSC + SC_FLAG] != 0.0;
-        sync();
         if (ok) return true;
         if (X.delta >= DELTA_MAX) return false;
         X.delta = X.delta > 0.0 ? 10.0 * X.delta : DELTA0;
@@ -979,22 +986,19 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const int N = X.N;
-    if (X.ln == 0) {
-        solve_core(X, Y.oGL, Y.oDZ);
-        double n0 = 0.0, n1 = 0.0;
-        if (X.fin) {
-            const double b0 = rE[0] - L[Y.oDZ + NZ * N + 0], b1 = rE[1] - L[Y.oDZ + NZ * N + 4];
-            const double e0 = L[Y.oSC + SC_EM0], e1 = L[Y.oSC + SC_EM1], e2 = L[Y.oSC + SC_EM2], e3 = L[Y.oSC + SC_EM3];
-            const double det = e0 * e3 - e1 * e2;
-            n0 = (b0 * e3 - e1 * b1) / det;
-            n1 = (e0 * b1 - e2 * b0) / det;
-        }
-        L[Y.oSC + SC_NU0] = n0;
-        L[Y.oSC + SC_NU1] = n1;
-    }
+    solve_core(X, Y.oGL, Y.oDZ);
     sync();
-    X.nu[0] = L[Y.oSC + SC_NU0];
-    X.nu[1] = L[Y.oSC + SC_NU1];
+    double n0 = 0.0, n1 = 0.0;
+    if (X.fin) {
+        const double b0 = rE[0] - L[Y.oDZ + NZ * N + 0], b1 = rE[1] - L[Y.oDZ + NZ * N + 4];
+        const double e0 = L[Y.oSC + SC_EM0], e1 = L[Y.oSC + SC_EM1], e2 = L[Y.oSC + SC_EM2], e3 = L[Y.oSC + SC_EM3];
+        const double det = e0 * e3 - e1 * e2;
+        n0 = (b0 * e3 - e1 * b1) / det;
+        n1 = (e0 * b1 - e2 * b0) / det;
+    }
+    X.nu[0] = n0;
+    X.nu[1] = n1;
+    sync();
     if (X.fin)
         for (int k = X.ln; k <= N; k += WAVE)
 #pragma unroll
@@ -1003,33 +1007,30 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     sync();
 }
 
-// dynamics-feasible start at oz (lane 0): dx_0 = xi0, dw = 0
+// dynamics-feasible start at oz: dx_0 = xi0, dw = 0 (the state recursion one entry per lane on lanes 0..4,
+// broadcast by readlane; lane 0 stores)
 __device__ void rollout(const Ctx& X, int oz) {
     PHASE(PH_ROLLOUT);
-    if (X.ln == 0) {
-        const int N = X.N;
-        ldsd* L = X.L;
-        const Layout& Y = X.Y;
-        double x[5];
+    const int N = X.N;
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+    const int me = X.ln < 5 ? X.ln : 0;
+    double x[5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) x[i] = X.xi0[i];
-        for (int k = 0; k <= N; ++k) {
+    for (int i = 0; i < 5; ++i) x[i] = X.xi0[i];
+    for (int k = 0; k <= N; ++k) {
+        if (X.ln == 0) {
 #pragma unroll
             for (int i = 0; i < 5; ++i) L[oz + NZ * k + i] = x[i];
 #pragma unroll
             for (int i = 5; i < NZ; ++i) L[oz + NZ * k + i] = 0.0;
-            if (k == N) break;
-            double xn[5];
-#pragma unroll
-            for (int i = 0; i < 5; ++i) {
-                double v = L[Y.oC + 5 * k + i];
-#pragma unroll
-                for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * i + l] * x[l];
-                xn[i] = v;
-            }
-#pragma unroll
-            for (int i = 0; i < 5; ++i) x[i] = xn[i];
         }
+        if (k == N) break;
+        double v = L[Y.oC + 5 * k + me];
+#pragma unroll
+        for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * me + l] * x[l];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x[i] = bcast(v, i);
     }
     sync();
 }
@@ -1068,12 +1069,11 @@ __device__ int eqp(Ctx& X, double scale) {
         for (int k = X.ln; k <= N; k += WAVE) {
             double g[NZ];
             grad_f(X, k, Y.oTZ, g);
-            int kinds[NR];
-            const int nr = stage_rows(k, N, X.fin, kinds);
+            const int nr = stage_nrows(k, N, X.fin);
             for (int j = 0; j < nr; ++j) {
                 if (!act_bit(X, Y.oTACT, k, j)) continue;
                 double a[NZ];
-                coef_of(X, k, kinds[j], a);
+                coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
                 const double f = RHO * row_val(X, k, j, a, Y.oTZ) - L[Y.oY + NR * k + j];
 #pragma unroll
                 for (int u = 0; u < NZ; ++u) g[u] += f * a[u];
@@ -1087,12 +1087,11 @@ __device__ int eqp(Ctx& X, double scale) {
         for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oTZ + NZ * k + u] += L[Y.oDZ + NZ * k + u];
-            int kinds[NR];
-            const int nr = stage_rows(k, N, X.fin, kinds);
+            const int nr = stage_nrows(k, N, X.fin);
             for (int j = 0; j < nr; ++j)
                 if (act_bit(X, Y.oTACT, k, j)) {
                     double a[NZ];
-                    coef_of(X, k, kinds[j], a);
+                    coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
                     L[Y.oY + NR * k + j] -= RHO * row_val(X, k, j, a, Y.oTZ);
                 }
         }
@@ -1104,12 +1103,11 @@ __device__ int eqp(Ctx& X, double scale) {
     for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oTZ + NZ * k + u]) ? fin : 0.0;
-        int kinds[NR];
-        const int nr = stage_rows(k, N, X.fin, kinds);
+        const int nr = stage_nrows(k, N, X.fin);
         unsigned mask = (unsigned)L[Y.oTACT + k];
         for (int j = 0; j < nr; ++j) {
             double a[NZ];
-            coef_of(X, k, kinds[j], a);
+            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
             const double rv = row_val(X, k, j, a, Y.oTZ);
             if ((mask >> j) & 1u) {
                 const double y = L[Y.oY + NR * k + j];
@@ -1138,11 +1136,10 @@ __device__ int ipm(Ctx& X, int* iters) {
     rollout(X, Y.oZ);
     int m = 0;
     for (int k = X.ln; k <= N; k += WAVE) {
-        int kinds[NR];
-        const int nr = stage_rows(k, N, X.fin, kinds);
+        const int nr = stage_nrows(k, N, X.fin);
         for (int j = 0; j < nr; ++j) {
             double a[NZ];
-            coef_of(X, k, kinds[j], a);
+            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
             const double rv = row_val(X, k, j, a, Y.oZ);
             L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
             L[Y.oLAM + NR * k + j] = 1.0;
@@ -1156,13 +1153,13 @@ __device__ int ipm(Ctx& X, int* iters) {
     for (; it < X.P.max_iter; ++it) {
         double mu = 0.0;
         for (int k = X.ln; k <= N; k += WAVE) {
-            int kinds[NR];
-            const int nr = stage_rows(k, N, X.fin, kinds);
+            const int nr = stage_nrows(k, N, X.fin);
             for (int j = 0; j < nr; ++j) mu += L[Y.oS + NR * k + j] * L[Y.oLAM + NR * k + j];
         }
         mu = wsum(mu) / m;
         if (!isfinite(mu)) { rc = -1; break; }
         if (mu <= X.P.tol && phi <= 1e-12) { rc = 0; break; }
+        if (X.dbg & 1) (void)factor_reg(X, 0);
         if (!factor_reg(X, 0)) { rc = -1; break; }
         const double rE[2] = {X.e[0] - L[Y.oZ + NZ * N + 0], X.e[1] - L[Y.oZ + NZ * N + 4]};
         for (int pass = 0; pass < 2; ++pass) {
@@ -1170,8 +1167,7 @@ __device__ int ipm(Ctx& X, int* iters) {
             if (pass == 1) {
                 double am = 1.0;
                 for (int k = X.ln; k <= N; k += WAVE) {
-                    int kinds[NR];
-                    const int nr = stage_rows(k, N, X.fin, kinds);
+                    const int nr = stage_nrows(k, N, X.fin);
                     for (int j = 0; j < nr; ++j) {
                         const double dsa = L[Y.oDSA + NR * k + j], dla = L[Y.oDLA + NR * k + j];
                         if (dsa < 0.0) am = fmin(am, -L[Y.oS + NR * k + j] / dsa);
@@ -1181,8 +1177,7 @@ __device__ int ipm(Ctx& X, int* iters) {
                 am = wmin(am);
                 double mua = 0.0;
                 for (int k = X.ln; k <= N; k += WAVE) {
-                    int kinds[NR];
-                    const int nr = stage_rows(k, N, X.fin, kinds);
+                    const int nr = stage_nrows(k, N, X.fin);
                     for (int j = 0; j < nr; ++j)
                         mua += (L[Y.oS + NR * k + j] + am * L[Y.oDSA + NR * k + j]) *
                                (L[Y.oLAM + NR * k + j] + am * L[Y.oDLA + NR * k + j]);
@@ -1191,14 +1186,14 @@ __device__ int ipm(Ctx& X, int* iters) {
                 const double ratio = mua / mu;
                 sigma_mu = ratio * ratio * ratio * mu;
             }
+            for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 2) & 1); ++rp_)
             for (int k = X.ln; k <= N; k += WAVE) {
                 double g[NZ];
                 grad_f(X, k, Y.oZ, g);
-                int kinds[NR];
-                const int nr = stage_rows(k, N, X.fin, kinds);
+                const int nr = stage_nrows(k, N, X.fin);
                 for (int j = 0; j < nr; ++j) {
                     double a[NZ];
-                    coef_of(X, k, kinds[j], a);
+                    coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
                     double rs = -s * l;
                     if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
@@ -1211,14 +1206,15 @@ __device__ int ipm(Ctx& X, int* iters) {
                 for (int u = 0; u < NZ; ++u) L[Y.oGL + NZ * k + u] = g[u];
             }
             sync();
+            if (X.dbg & 2) solve(X, rE);
             solve(X, rE);
             const int ods = pass == 0 ? Y.oDSA : Y.oDS, odl = pass == 0 ? Y.oDLA : Y.oDL;
+            for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 3) & 1); ++rp_)
             for (int k = X.ln; k <= N; k += WAVE) {
-                int kinds[NR];
-                const int nr = stage_rows(k, N, X.fin, kinds);
+                const int nr = stage_nrows(k, N, X.fin);
                 for (int j = 0; j < nr; ++j) {
                     double a[NZ];
-                    coef_of(X, k, kinds[j], a);
+                    coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
                     double rs = -s * l;
                     if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
@@ -1233,8 +1229,7 @@ __device__ int ipm(Ctx& X, int* iters) {
         }
         double amax = 1.0 / TAU, fin = 1.0;
         for (int k = X.ln; k <= N; k += WAVE) {
-            int kinds[NR];
-            const int nr = stage_rows(k, N, X.fin, kinds);
+            const int nr = stage_nrows(k, N, X.fin);
             for (int j = 0; j < nr; ++j) {
                 const double ds = L[Y.oDS + NR * k + j], dl = L[Y.oDL + NR * k + j];
                 if (ds < 0.0) amax = fmin(amax, -L[Y.oS + NR * k + j] / ds);
@@ -1250,8 +1245,7 @@ __device__ int ipm(Ctx& X, int* iters) {
         for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oZ + NZ * k + u] += alpha * L[Y.oDZ + NZ * k + u];
-            int kinds[NR];
-            const int nr = stage_rows(k, N, X.fin, kinds);
+            const int nr = stage_nrows(k, N, X.fin);
             for (int j = 0; j < nr; ++j) {
                 L[Y.oS + NR * k + j] += alpha * L[Y.oDS + NR * k + j];
                 L[Y.oLAM + NR * k + j] += alpha * L[Y.oDL + NR * k + j];
@@ -1281,8 +1275,7 @@ __device__ void accept_polish(const Ctx& X, bool with_act) {
 
 // interior-point classification (s < lam) of stage k as a bit mask
 __device__ double ipm_mask(const Ctx& X, int k) {
-    int kinds[NR];
-    const int nr = stage_rows(k, X.N, X.fin, kinds);
+    const int nr = stage_nrows(k, X.N, X.fin);
     unsigned m = 0;
     for (int j = 0; j < nr; ++j)
         if (X.L[X.Y.oS + NR * k + j] < X.L[X.Y.oLAM + NR * k + j]) m |= 1u << j;
@@ -1296,8 +1289,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
     const Layout& Y = X.Y;
     double scale = 1.0;
     for (int k = X.ln; k <= N; k += WAVE) {
-        int kinds[NR];
-        const int nr = stage_rows(k, N, X.fin, kinds);
+        const int nr = stage_nrows(k, N, X.fin);
         for (int j = 0; j < nr; ++j) scale = fmax(scale, fabs(L[Y.oG + NR * k + j]));
     }
     scale = wmax(scale);
@@ -1348,25 +1340,25 @@ __device__ void multipliers(Ctx& X) {
     for (int k = X.ln; k <= N; k += WAVE) {
         double g[NZ];
         grad_f(X, k, Y.oZ, g);
-        int kinds[NR];
-        const int nr = stage_rows(k, N, X.fin, kinds);
+        const int nr = stage_nrows(k, N, X.fin);
         L[Y.oMLAT + 2 * k] = 0.0;
         L[Y.oMLAT + 2 * k + 1] = 0.0;
         for (int j = 0; j < nr; ++j) {
             double a[NZ];
-            coef_of(X, k, kinds[j], a);
+            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
             const double l = L[Y.oLAM + NR * k + j];
 #pragma unroll
             for (int u = 0; u < NZ; ++u) g[u] -= l * a[u];
-            if (kinds[j] == ROW_LATP) L[Y.oMLAT + 2 * k] = l;
-            if (kinds[j] == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
+            if (row_kind(k, X.N, X.fin, j) == ROW_LATP) L[Y.oMLAT + 2 * k] = l;
+            if (row_kind(k, X.N, X.fin, j) == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
         }
 #pragma unroll
         for (int u = 0; u < 5; ++u) L[Y.oGL + NZ * k + u] = g[u];
     }
     sync();
-    // co-states (lane 0): PI[k] = pi_{k+1}
-    if (X.ln == 0) {
+    // co-states: PI[k] = pi_{k+1} (one entry per lane on lanes 0..4, broadcast by readlane; lane 0 stores)
+    {
+        const int me = X.ln < 5 ? X.ln : 0;
         double pi[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) pi[i] = L[Y.oGL + NZ * N + i];
@@ -1375,19 +1367,15 @@ __device__ void multipliers(Ctx& X) {
             pi[4] += X.nu[1];
         }
         for (int k = N - 1; k >= 0; --k) {
+            if (X.ln == 0)
 #pragma unroll
-            for (int i = 0; i < 5; ++i) L[Y.oPI + 5 * k + i] = pi[i];
+                for (int i = 0; i < 5; ++i) L[Y.oPI + 5 * k + i] = pi[i];
             if (k > 0) {
-                double pn[5];
+                double v = L[Y.oGL + NZ * k + me];
 #pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    double v = L[Y.oGL + NZ * k + i];
+                for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + me] * pi[l];
 #pragma unroll
-                    for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + i] * pi[l];
-                    pn[i] = v;
-                }
-#pragma unroll
-                for (int i = 0; i < 5; ++i) pi[i] = pn[i];
+                for (int i = 0; i < 5; ++i) pi[i] = bcast(v, i);
             }
         }
     }
@@ -1491,7 +1479,7 @@ __device__ inline ldsd* lds_p(const Ctx& X) { return X.L; }
 struct KArgs {
     DevRoute R;
     plan_params P;
-    int B, Nmax, Nfixed;
+    int B, Nmax, Nfixed, dbg;
     const int* N;
     const double *x0, *st;
     const int* fin;
@@ -1508,6 +1496,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
     X.Y = make_layout(a.Nmax);
     X.L = (ldsd*)lds;
     X.ln = threadIdx.x;
+    X.dbg = a.dbg;
     X.N = a.N ? a.N[b] : a.Nfixed;
     const int N = X.N;
     X.fin = a.fin ? (a.fin[b] != 0) : 0;
@@ -1544,6 +1533,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         bool exact = last <= EXACT_STEP;
         int rc = -1;
         for (;;) {
+            if (X.dbg & 16) (void)build_qp(X, frozen, exact);
             if (!build_qp(X, frozen, exact)) { rc = -2; break; }
             int ni = 0;
             rc = qp_solve(X, have_cls, &ni);
@@ -1555,6 +1545,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         if (rc == -2) { status = PLAN_NUMERICAL; break; }
         if (rc < 0) { status = PLAN_QP_FAILED; break; }
         have_cls = true;
+        if (X.dbg & 32) multipliers(X);
         multipliers(X);
         double full = 0.0, mu_l = 0.0;
         for (int k = X.ln; k <= N; k += WAVE) {
@@ -1567,8 +1558,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
             if (k < N)
 #pragma unroll
                 for (int i = 0; i < 5; ++i) mu_l = fmax(mu_l, 2.0 * fabs(L[Y.oMY + 5 * k + i]));
-            int kinds[NR];
-            const int nr = stage_rows(k, N, X.fin, kinds);
+            const int nr = stage_nrows(k, N, X.fin);
             for (int j = 0; j < nr; ++j) mu_l = fmax(mu_l, 2.0 * fabs(L[Y.oLAM + NR * k + j]));
         }
         full = wmax(full);
@@ -1589,6 +1579,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
             for (int i = 0; i < (nh < LS_MEMORY ? nh : LS_MEMORY); ++i) m0 = fmax(m0, hf[i] + mu_m * hv[i]);
             for (int ls = 0; ls < LS_STEPS; ++ls) {
                 double f1, v1;
+                if (X.dbg & 64) cost_viol(X, alpha, &f1, &v1);
                 cost_viol(X, alpha, &f1, &v1);
                 if (f1 + mu_m * v1 <= m0 + LS_ARMIJO * alpha * dd || ls == LS_STEPS - 1) break;
                 alpha *= 0.5;

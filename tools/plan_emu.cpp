@@ -52,6 +52,16 @@ static inline int __shfl_xor(int v, int o, int) {
     return r;
 }
 
+// readlane: every lane gets lane src's value
+static inline double bcast(double v, int src) {
+    g_xd[threadIdx.x] = v;
+    pthread_barrier_wait(&g_bar);
+    const double r = g_xd[src];
+    pthread_barrier_wait(&g_bar);
+    return r;
+}
+#define PLAN_HOST_EMU 1
+
 #include "../safe-autonomous-driving-mpc_amd/csrc/plan_kernel.h"
 
 struct LaneArg {
@@ -113,6 +123,7 @@ int main(int argc, char** argv) {
     a.B = B;
     a.Nmax = Nmax;
     a.Nfixed = P.N;
+    a.dbg = 0;
     a.N = hasN ? Nv.data() : nullptr;
     a.x0 = x0.data();
     a.st = st.data();
