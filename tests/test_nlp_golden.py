@@ -53,7 +53,7 @@ def test_nlp_golden_coverage():
         assert k["prim"] <= 1e-9 and k["err_est"] <= 1e-6
 
 
-MAX_OTHER_OPTIMA = 2   # certified cases where the SQP may converge to a different local optimum
+MAX_OTHER_OPTIMA = 1   # certified cases where the SQP may converge to a different local optimum (case 34)
 
 
 def classify(U, U_cap_more, c, feasible_fn):
@@ -197,3 +197,38 @@ def test_oracle_closed_loop_traj2_long_horizon(N):
     print(f"traj2 N={N} FSM: {len(hu)} steps")
     assert len(hu) < 3000
     assert "===> Checks passed : True" in buf.getvalue(), buf.getvalue()[-600:]
+
+
+def test_second_start_on_the_other_optima(oracles):
+    """the certified cases where the drop-in SQP lands on another local optimum (case 34:
+    trajectory3, N=30, two obstacles) re-solved from a second start, the unbraked reference controls (the
+    warm start of :224-246 without the obstacle braking), keeping the lower reference cost.  Measured: from
+    that start the SQP converges (status 0, stops moving) at cost 112.2747, against 120.8911 from the braked
+    start and 112.2721 at the golden optimum SLSQP's path reached, yet 5e-2 away from it in U: a third local
+    optimum of the non-convex problem, 0.002% above the golden cost.  So the two-start rule recovers the
+    cost but not the point; MAX_OTHER_OPTIMA stays at the one such case, and the product keeps one start
+    (a second SQP would double every solve for 1 of 52 certified cases)."""
+    import oracle as O
+    import trajectory_tracking as TT
+    seen = 0
+    for j, c in enumerate(nlp_cases()):
+        if not bool(c["certified"]):
+            continue
+        orc, ob = oracles[int(c["traj"])], c["obs"]
+        o = ob if len(ob) else None
+        p = O.default_params(N=int(c["N"]), max_obs=len(ob), sqp_iters=TT.SQP_ITERS)
+        r1 = orc.solve(p, c["x0"], o)
+        if float(np.abs(r1["U"] - c["U_nlp"].ravel()).max()) <= TOL_NLP_MEAS:
+            continue
+        seen += 1
+        r2 = orc.solve(p, c["x0"], o, ubar=orc.warm_start(p, c["x0"], None).reshape(-1, 2))
+        f1, f2, fg = (orc.cost(p, c["x0"], U) for U in (r1["U"], r2["U"], c["U_nlp"]))
+        best = r2 if f2 < f1 else r1
+        fb = min(f1, f2)
+        e = float(np.abs(best["U"] - c["U_nlp"].ravel()).max())
+        print(f"case {j}: braked start cost {f1:.4f}, unbraked start cost {f2:.4f}, golden {fg:.4f}; "
+              f"best |U - U_nlp| = {e:.2e}")
+        assert best["status"] == 0
+        assert orc.constraints(p, c["x0"], o, best["U"]).min() >= -1e-9
+        assert fb <= fg * (1 + 1e-4), (j, fb, fg)
+    assert seen <= MAX_OTHER_OPTIMA
