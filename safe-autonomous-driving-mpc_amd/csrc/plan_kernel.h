@@ -336,24 +336,58 @@ __device__ inline int row_kind(int k, int N, int fin, int j) {
     return ROW_STERM;
 }
 
-// coefficients of a row over (x_k, w_k), at the SQP iterate's (k, v) of stage k
-__device__ void row_coef(int kind, bool has_w, double kb, double vb, double a[NZ]) {
-#pragma unroll
-    for (int u = 0; u < NZ; ++u) a[u] = 0.0;
+// Row coefficients over (x_k, w_k) at the SQP iterate's (k, v) of stage k, sparse: every row touches one or
+// two of the 8 stage variables, so instead of a dense 8-vector the loops visit the 12 row kinds in a fully
+// unrolled loop
+// (for_rows), where each kind, and with it the indices of its nonzero coefficients, is a compile-time
+// constant.  Adding only the nonzero terms, in the same order, gives the dense loops' values (a skipped
+// term is an exact zero).
+__device__ inline bool row_on(int kind, int k, int N, int fin) {
     switch (kind) {
-        case ROW_VMIN: a[4] = 1.0; a[7] = has_w ? 1.0 : 0.0; break;
-        case ROW_VMAX: a[4] = -1.0; a[7] = has_w ? -1.0 : 0.0; break;
-        case ROW_LATP: a[3] = -vb * vb; a[4] = -2.0 * kb * vb; break;
-        case ROW_LATM: a[3] = vb * vb; a[4] = 2.0 * kb * vb; break;
-        case ROW_KMIN: a[3] = 1.0; break;
-        case ROW_KMAX: a[3] = -1.0; break;
-        case ROW_U1MIN: a[5] = 1.0; break;
-        case ROW_U1MAX: a[5] = -1.0; break;
-        case ROW_U2MIN: a[6] = 1.0; break;
-        case ROW_U2MAX: a[6] = -1.0; break;
-        case ROW_S: a[7] = 1.0; break;
-        default: a[0] = 1.0; break;                              // ROW_STERM
+        case ROW_VMIN: case ROW_VMAX: return !(fin && k == N);
+        case ROW_LATP: case ROW_LATM: return !(fin && k == N) && k > 0;
+        case ROW_KMIN: case ROW_KMAX: return k > 0;
+        case ROW_STERM: return k == N && !fin;
+        default: return k < N;
     }
+}
+struct RowSp {
+    int i0, i1;          // indices of the coefficients (i0 < i1)
+    double c0, c1;
+    bool two;            // c1 present
+};
+__device__ inline RowSp row_sp(int kind, bool has_w, double kb, double vb) {
+    switch (kind) {
+        case ROW_VMIN: return {4, 7, 1.0, 1.0, has_w};
+        case ROW_VMAX: return {4, 7, -1.0, -1.0, has_w};
+        case ROW_LATP: return {3, 4, -vb * vb, -2.0 * kb * vb, true};
+        case ROW_LATM: return {3, 4, vb * vb, 2.0 * kb * vb, true};
+        case ROW_KMIN: return {3, 3, 1.0, 0.0, false};
+        case ROW_KMAX: return {3, 3, -1.0, 0.0, false};
+        case ROW_U1MIN: return {5, 5, 1.0, 0.0, false};
+        case ROW_U1MAX: return {5, 5, -1.0, 0.0, false};
+        case ROW_U2MIN: return {6, 6, 1.0, 0.0, false};
+        case ROW_U2MAX: return {6, 6, -1.0, 0.0, false};
+        case ROW_S: return {7, 7, 1.0, 0.0, false};
+        default: return {0, 0, 1.0, 0.0, false};        // ROW_STERM
+    }
+}
+// f(kind, j) for the rows of stage k in storage order (j = the row's slot)
+template <class F>
+__device__ inline void for_rows(int k, int N, int fin, F&& f) {
+    int j = 0;
+#pragma unroll
+    for (int kind = 0; kind <= ROW_STERM; ++kind)
+        if (row_on(kind, k, N, fin)) {
+            f(kind, j);
+            ++j;
+        }
+}
+// g + a . z
+__device__ inline double sp_dot(const RowSp& r, double g, const double z[NZ]) {
+    double v = g + r.c0 * z[r.i0];
+    if (r.two) v += r.c1 * z[r.i1];
+    return v;
 }
 
 // Gaussian elimination with partial pivoting on a 5x5 system with NC right-hand sides (registers)
@@ -458,17 +492,6 @@ struct PhScope {
 #else
 #define PHASE(p)
 #endif
-
-__device__ inline void coef_of(const Ctx& X, int k, int kind, double a[NZ]) {
-    row_coef(kind, k < X.N, X.L[X.Y.oZB + NZ * k + 3], X.L[X.Y.oZB + NZ * k + 4], a);
-}
-
-__device__ inline double row_val(const Ctx& X, int k, int j, const double a[NZ], int oz) {
-    double v = X.L[X.Y.oG + NR * k + j];
-#pragma unroll
-    for (int u = 0; u < NZ; ++u) v += a[u] * X.L[oz + NZ * k + u];
-    return v;
-}
 
 __device__ inline bool act_bit(const Ctx& X, int o, int k, int j) {
     return (((unsigned)X.L[o + k]) >> j) & 1u;
@@ -753,17 +776,18 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
 #pragma unroll
         for (int i = 0; i < NZ; ++i)
             if (i < nv) H[hx(i, i)] += X.delta;
-        const int nr = stage_nrows(k, N, X.fin);
-        for (int j = 0; j < nr; ++j) {
-            const double w = mode == 0 ? L[Y.oLAM + NR * k + j] / L[Y.oS + NR * k + j] : (act_bit(X, Y.oTACT, k, j) ? RHO : 0.0);
-            if (w == 0.0) continue;
-            double a[NZ];
-            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
-#pragma unroll
-            for (int u = 0; u < NZ; ++u)
-#pragma unroll
-                for (int v = u; v < NZ; ++v) H[hx(u, v)] += w * a[u] * a[v];
-        }
+        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        const unsigned act = mode == 0 ? 0u : (unsigned)L[Y.oTACT + k];
+        for_rows(k, N, X.fin, [&](int kind, int j) {
+            const double w = mode == 0 ? L[Y.oLAM + NR * k + j] / L[Y.oS + NR * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
+            if (w == 0.0) return;
+            const RowSp r = row_sp(kind, k < N, kb, vb);
+            H[hx(r.i0, r.i0)] += w * r.c0 * r.c0;
+            if (r.two) {
+                H[hx(r.i0, r.i1)] += w * r.c0 * r.c1;
+                H[hx(r.i1, r.i1)] += w * r.c1 * r.c1;
+            }
+        });
 #pragma unroll
         for (int i = 0; i < NH; ++i) L[Y.oHT + NH * k + i] = H[i];
     }
@@ -1067,17 +1091,19 @@ __device__ int eqp(Ctx& X, double scale) {
     rollout(X, Y.oTZ);
     for (int it = 0; it < AL_STEPS; ++it) {
         for (int k = X.ln; k <= N; k += WAVE) {
-            double g[NZ];
+            double g[NZ], z[NZ];
             grad_f(X, k, Y.oTZ, g);
-            const int nr = stage_nrows(k, N, X.fin);
-            for (int j = 0; j < nr; ++j) {
-                if (!act_bit(X, Y.oTACT, k, j)) continue;
-                double a[NZ];
-                coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
-                const double f = RHO * row_val(X, k, j, a, Y.oTZ) - L[Y.oY + NR * k + j];
 #pragma unroll
-                for (int u = 0; u < NZ; ++u) g[u] += f * a[u];
-            }
+            for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + NZ * k + u];
+            const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+            const unsigned act = (unsigned)L[Y.oTACT + k];
+            for_rows(k, N, X.fin, [&](int kind, int j) {
+                if (!((act >> j) & 1u)) return;
+                const RowSp r = row_sp(kind, k < N, kb, vb);
+                const double f = RHO * sp_dot(r, L[Y.oG + NR * k + j], z) - L[Y.oY + NR * k + j];
+                g[r.i0] += f * r.c0;
+                if (r.two) g[r.i1] += f * r.c1;
+            });
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oGL + NZ * k + u] = g[u];
         }
@@ -1087,13 +1113,15 @@ __device__ int eqp(Ctx& X, double scale) {
         for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oTZ + NZ * k + u] += L[Y.oDZ + NZ * k + u];
-            const int nr = stage_nrows(k, N, X.fin);
-            for (int j = 0; j < nr; ++j)
-                if (act_bit(X, Y.oTACT, k, j)) {
-                    double a[NZ];
-                    coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
-                    L[Y.oY + NR * k + j] -= RHO * row_val(X, k, j, a, Y.oTZ);
-                }
+            double z[NZ];
+#pragma unroll
+            for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + NZ * k + u];
+            const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+            const unsigned act = (unsigned)L[Y.oTACT + k];
+            for_rows(k, N, X.fin, [&](int kind, int j) {
+                if ((act >> j) & 1u)
+                    L[Y.oY + NR * k + j] -= RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
+            });
         }
         sync();
     }
@@ -1103,12 +1131,13 @@ __device__ int eqp(Ctx& X, double scale) {
     for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oTZ + NZ * k + u]) ? fin : 0.0;
-        const int nr = stage_nrows(k, N, X.fin);
         unsigned mask = (unsigned)L[Y.oTACT + k];
-        for (int j = 0; j < nr; ++j) {
-            double a[NZ];
-            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
-            const double rv = row_val(X, k, j, a, Y.oTZ);
+        double z[NZ];
+#pragma unroll
+        for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + NZ * k + u];
+        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        for_rows(k, N, X.fin, [&](int kind, int j) {
+            const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
             if ((mask >> j) & 1u) {
                 const double y = L[Y.oY + NR * k + j];
                 L[Y.oTLAM + NR * k + j] = y;
@@ -1117,7 +1146,7 @@ __device__ int eqp(Ctx& X, double scale) {
                 L[Y.oTLAM + NR * k + j] = 0.0;
                 if (rv < -tr) { mask |= 1u << j; ++bad; }
             }
-        }
+        });
         L[Y.oTACT + k] = (double)mask;
     }
     fin = wmin(fin);
@@ -1136,15 +1165,16 @@ __device__ int ipm(Ctx& X, int* iters) {
     rollout(X, Y.oZ);
     int m = 0;
     for (int k = X.ln; k <= N; k += WAVE) {
-        const int nr = stage_nrows(k, N, X.fin);
-        for (int j = 0; j < nr; ++j) {
-            double a[NZ];
-            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
-            const double rv = row_val(X, k, j, a, Y.oZ);
+        double z[NZ];
+#pragma unroll
+        for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + NZ * k + u];
+        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        for_rows(k, N, X.fin, [&](int kind, int j) {
+            const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
             L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
             L[Y.oLAM + NR * k + j] = 1.0;
             ++m;
-        }
+        });
     }
     m = wsumi(m);
     sync();
@@ -1188,20 +1218,21 @@ __device__ int ipm(Ctx& X, int* iters) {
             }
             for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 2) & 1); ++rp_)
             for (int k = X.ln; k <= N; k += WAVE) {
-                double g[NZ];
+                double g[NZ], z[NZ];
                 grad_f(X, k, Y.oZ, g);
-                const int nr = stage_nrows(k, N, X.fin);
-                for (int j = 0; j < nr; ++j) {
-                    double a[NZ];
-                    coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
+#pragma unroll
+                for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + NZ * k + u];
+                const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+                for_rows(k, N, X.fin, [&](int kind, int j) {
+                    const RowSp r = row_sp(kind, k < N, kb, vb);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
                     double rs = -s * l;
                     if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
-                    const double rp = row_val(X, k, j, a, Y.oZ) - s;
+                    const double rp = sp_dot(r, L[Y.oG + NR * k + j], z) - s;
                     const double f = l + (rs - l * rp) / s;
-#pragma unroll
-                    for (int u = 0; u < NZ; ++u) g[u] -= f * a[u];
-                }
+                    g[r.i0] -= f * r.c0;
+                    if (r.two) g[r.i1] -= f * r.c1;
+                });
 #pragma unroll
                 for (int u = 0; u < NZ; ++u) L[Y.oGL + NZ * k + u] = g[u];
             }
@@ -1211,19 +1242,24 @@ __device__ int ipm(Ctx& X, int* iters) {
             const int ods = pass == 0 ? Y.oDSA : Y.oDS, odl = pass == 0 ? Y.oDLA : Y.oDL;
             for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 3) & 1); ++rp_)
             for (int k = X.ln; k <= N; k += WAVE) {
-                const int nr = stage_nrows(k, N, X.fin);
-                for (int j = 0; j < nr; ++j) {
-                    double a[NZ];
-                    coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
+                double z[NZ], dz[NZ];
+#pragma unroll
+                for (int u = 0; u < NZ; ++u) {
+                    z[u] = L[Y.oZ + NZ * k + u];
+                    dz[u] = L[Y.oDZ + NZ * k + u];
+                }
+                const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+                for_rows(k, N, X.fin, [&](int kind, int j) {
+                    const RowSp r = row_sp(kind, k < N, kb, vb);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
                     double rs = -s * l;
                     if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
-                    double v = row_val(X, k, j, a, Y.oZ) - s;
-#pragma unroll
-                    for (int u = 0; u < NZ; ++u) v += a[u] * L[Y.oDZ + NZ * k + u];
+                    double v = sp_dot(r, L[Y.oG + NR * k + j], z) - s;
+                    v += r.c0 * dz[r.i0];
+                    if (r.two) v += r.c1 * dz[r.i1];
                     L[ods + NR * k + j] = v;
                     L[odl + NR * k + j] = (rs - l * v) / s;
-                }
+                });
             }
             sync();
         }
@@ -1340,18 +1376,17 @@ __device__ void multipliers(Ctx& X) {
     for (int k = X.ln; k <= N; k += WAVE) {
         double g[NZ];
         grad_f(X, k, Y.oZ, g);
-        const int nr = stage_nrows(k, N, X.fin);
         L[Y.oMLAT + 2 * k] = 0.0;
         L[Y.oMLAT + 2 * k + 1] = 0.0;
-        for (int j = 0; j < nr; ++j) {
-            double a[NZ];
-            coef_of(X, k, row_kind(k, X.N, X.fin, j), a);
+        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        for_rows(k, N, X.fin, [&](int kind, int j) {
+            const RowSp r = row_sp(kind, k < N, kb, vb);
             const double l = L[Y.oLAM + NR * k + j];
-#pragma unroll
-            for (int u = 0; u < NZ; ++u) g[u] -= l * a[u];
-            if (row_kind(k, X.N, X.fin, j) == ROW_LATP) L[Y.oMLAT + 2 * k] = l;
-            if (row_kind(k, X.N, X.fin, j) == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
-        }
+            g[r.i0] -= l * r.c0;
+            if (r.two) g[r.i1] -= l * r.c1;
+            if (kind == ROW_LATP) L[Y.oMLAT + 2 * k] = l;
+            if (kind == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
+        });
 #pragma unroll
         for (int u = 0; u < 5; ++u) L[Y.oGL + NZ * k + u] = g[u];
     }
