@@ -59,7 +59,7 @@ def main():
                     help="also run B egos per GPU through the device closed loop (mpc_closed_loop, SURVEY 8(f)1) "
                          "on the config's trajectory and FSM preset, gather their check quantities to rank 0 and "
                          "report closed-loop ego-steps/s (0: skip)")
-    ap.add_argument("--plan-chunks", type=int, default=16384, metavar="B",
+    ap.add_argument("--plan-chunks", type=int, default=65536, metavar="B",
                     help="offline-planner leg (SURVEY 8(f)4, libmpcplan): B chunk NLPs per GPU posed as "
                          "optimize_full_trajectory poses them (20 m chunks, per-chunk horizon) on --plan-route; "
                          "reported as 'plan' in chunks/s, never as 'value' (0: skip)")

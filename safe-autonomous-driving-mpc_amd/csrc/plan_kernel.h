@@ -807,58 +807,109 @@ __device__ inline double bcast(double v, int src) {
 // solve, feedback) are computed by every lane alike, and the 5-vectors of the recursions (co-state p
 // backwards, state x forwards) one entry per lane on lanes 0..4 and broadcast by readlane.  Every entry
 // is formed by the same operations in the same order as on one lane, so the result is the same.
+// stage records of the two sweeps, loaded one stage ahead (software pipelining: the LDS latency of stage
+// k - 1's data overlaps stage k's arithmetic)
+struct BwdRec {
+    double Lc[6], B0[5], B1[5], gw[3], gx, Acol[5], Kcol[3];
+};
+struct FwdRec {
+    double K[15], Arow[5], Brow[2];
+};
+__device__ inline void load_bwd(const Ctx& X, int ogl, int k, int me, BwdRec& R) {
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) R.Lc[i] = L[Y.oL + 6 * k + i];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        R.B0[l] = L[Y.oB + 10 * k + 2 * l];
+        R.B1[l] = L[Y.oB + 10 * k + 2 * l + 1];
+        R.Acol[l] = L[Y.oA + 25 * k + 5 * l + me];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        R.gw[i] = L[ogl + NZ * k + 5 + i];
+        R.Kcol[i] = L[Y.oK + 15 * k + 5 * i + me];
+    }
+    R.gx = L[ogl + NZ * k + me];
+}
+__device__ inline void load_fwd(const Ctx& X, int k, int me, FwdRec& R) {
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) R.K[i] = L[Y.oK + 15 * k + i];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) R.Arow[l] = L[Y.oA + 25 * k + 5 * me + l];
+    R.Brow[0] = L[Y.oB + 10 * k + 2 * me];
+    R.Brow[1] = L[Y.oB + 10 * k + 2 * me + 1];
+}
+#ifndef PLAN_HOST_EMU
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SCHED_FENCE()
+#endif
+
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     const int N = X.N;
     ldsd* L = X.L;
-    const Layout& Y = X.Y;
     const int me = X.ln < 5 ? X.ln : 0;
     double p[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = L[ogl + NZ * N + i];
+    BwdRec cur, nxt;
+    load_bwd(X, ogl, N - 1, me, cur);
     for (int k = N - 1; k >= 0; --k) {
-        double h[3], Lc[6];
+        load_bwd(X, ogl, k > 0 ? k - 1 : 0, me, nxt);
+        SCHED_FENCE();
+        double h[3];
+        {
+            double v = cur.gw[0];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) Lc[i] = L[Y.oL + 6 * k + i];
+            for (int l = 0; l < 5; ++l) v += cur.B0[l] * p[l];
+            h[0] = v;
+            v = cur.gw[1];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            double v = L[ogl + NZ * k + 5 + i];
-#pragma unroll
-            for (int l = 0; l < 5; ++l) v += L[Y.oB + 10 * k + 2 * l + i] * p[l];
-            h[i] = v;
+            for (int l = 0; l < 5; ++l) v += cur.B1[l] * p[l];
+            h[1] = v;
         }
-        h[2] = L[ogl + NZ * k + 7];
+        h[2] = cur.gw[2];
         double t[3] = {-h[0], -h[1], -h[2]};
-        chol3_solve(Lc, t);
+        chol3_solve(cur.Lc, t);
         if (X.ln == 0)
 #pragma unroll
             for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = t[i];
         if (k > 0) {
-            double v = L[ogl + NZ * k + me];
+            double v = cur.gx;
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + me] * p[l];
+            for (int l = 0; l < 5; ++l) v += cur.Acol[l] * p[l];
 #pragma unroll
-            for (int l = 0; l < 3; ++l) v += L[Y.oK + 15 * k + 5 * l + me] * h[l];
+            for (int l = 0; l < 3; ++l) v += cur.Kcol[l] * h[l];
 #pragma unroll
             for (int i = 0; i < 5; ++i) p[i] = bcast(v, i);
         }
+        cur = nxt;
     }
     // the forward pass reads the control parts just stored
     sync();
     double x[5] = {0, 0, 0, 0, 0};
+    FwdRec fc, fn;
+    load_fwd(X, 0, me, fc);
     for (int k = 0; k < N; ++k) {
+        load_fwd(X, k + 1 < N ? k + 1 : k, me, fn);
+        SCHED_FENCE();
         double w[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             double v = L[odz + NZ * k + 5 + i];
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v += L[Y.oK + 15 * k + 5 * i + l] * x[l];
+            for (int l = 0; l < 5; ++l) v += fc.K[5 * i + l] * x[l];
             w[i] = v;
         }
         double v = 0.0;
 #pragma unroll
-        for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * me + l] * x[l];
+        for (int l = 0; l < 5; ++l) v += fc.Arow[l] * x[l];
 #pragma unroll
-        for (int l = 0; l < 2; ++l) v += L[Y.oB + 10 * k + 2 * me + l] * w[l];
+        for (int l = 0; l < 2; ++l) v += fc.Brow[l] * w[l];
         // stage k overwritten after every lane has read its control part (the broadcast orders that)
         double xn[5];
 #pragma unroll
@@ -871,6 +922,7 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) x[i] = xn[i];
+        fc = fn;
     }
     if (X.ln == 0) {
 #pragma unroll

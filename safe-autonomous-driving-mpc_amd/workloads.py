@@ -148,29 +148,32 @@ def plan_batch_ref(route, B, seed=0, chunk=20.0, final_frac=0.1, offset=0):
     """B chunks on `route` as optimize_full_trajectory (trajectory_planning.py:491-515) poses them with its
     default max_chunk_size = 20 m: an intermediate chunk spans D = chunk metres from s0, the final one the
     remaining D ~ U(1.5, 2) chunk to the destination (the loop's last chunk, remaining < 2 chunk), and each
-    gets its own horizon N = ceil(2 D / avg_speed(s0) / 0.3).  Start states as plan_batch.  Returns
-    dict(x0 [B,5], s_target [B], is_final [B] int32, N [B] int32), sorted by N (one launch per horizon)."""
+    gets its own horizon N = ceil(2 D / avg_speed(s0) / 0.3).  Start states as plan_batch.  Vectorised over
+    the batch (the route functions evaluated on arrays, avg_speed once per 5 m cell).  Returns dict(x0
+    [B,5], s_target [B], is_final [B] int32, N [B] int32), sorted by N (one launch per horizon)."""
     rs = [np.random.default_rng(c) for c in np.random.SeedSequence(seed).spawn(7)]
+    sl = slice(offset, offset + B)
     tot = offset + B
-    u0, nd, no, uv, uf, ud = (rs[0].uniform(0, 1, tot), rs[1].normal(0, 0.05, tot), rs[2].normal(0, 0.01, tot),
-                              rs[3].uniform(0.2, 0.9, tot), rs[4].uniform(0, 1, tot), rs[5].uniform(1.5, 2.0, tot))
-    x0 = np.empty((B, 5))
-    st = np.empty(B)
-    fin = np.zeros(B, np.int32)
-    Nv = np.empty(B, np.int32)
-    for b in range(B):
-        i = offset + b
-        if uf[i] < final_frac:
-            D = min(ud[i] * chunk, route.s_total - 1.0)
-            s0 = route.s_total - D
-            vmax = min(route.v_max_fun(s0), np.sqrt(2.0 * 2.5 * D))
-            fin[b] = 1
-        else:
-            D = chunk
-            s0 = 1.0 + u0[i] * (route.s_total - 2.0 * chunk - 2.0)
-            vmax = route.v_max_fun(s0)
-        x0[b] = (s0, nd[i], no[i], route.k_ref_fun(s0), uv[i] * vmax)
-        st[b] = s0 + D if not fin[b] else route.s_total
-        Nv[b] = int(np.ceil(D / route.avg_speed_from(s0) * 2.0 / 0.3))
+    u0, nd, no, uv, uf, ud = (rs[0].uniform(0, 1, tot)[sl], rs[1].normal(0, 0.05, tot)[sl],
+                              rs[2].normal(0, 0.01, tot)[sl], rs[3].uniform(0.2, 0.9, tot)[sl],
+                              rs[4].uniform(0, 1, tot)[sl], rs[5].uniform(1.5, 2.0, tot)[sl])
+    fin = (uf < final_frac).astype(np.int32)
+    Df = np.minimum(ud * chunk, route.s_total - 1.0)
+    s0 = np.where(fin == 1, route.s_total - Df, 1.0 + u0 * (route.s_total - 2.0 * chunk - 2.0))
+    D = np.where(fin == 1, Df, chunk)
+    vm = np.asarray(route._vint(s0), np.float64)
+    vmax = np.where(fin == 1, np.minimum(vm, np.sqrt(2.0 * 2.5 * D)), vm)
+    t = np.asarray(route._s_to_t(s0), np.float64)
+    xs, ys = route.spline
+    x1, y1, x2, y2 = xs(t, 1), ys(t, 1), xs(t, 2), ys(t, 2)
+    den = (x1 ** 2 + y1 ** 2) ** 1.5 + 1e-9
+    den = np.where(den < 1e-8, 1e-8, den)
+    k0 = (x1 * y2 - y1 * x2) / den
+    cells = (s0 / 5).astype(int)
+    avg = {c: route.avg_speed_from(5.0 * c) for c in np.unique(cells)}
+    av = np.array([avg[c] for c in cells])
+    Nv = np.ceil(D / av * 2.0 / 0.3).astype(np.int32)
+    x0 = np.stack([s0, nd, no, k0, uv * vmax], axis=1)
+    st = np.where(fin == 1, route.s_total, s0 + D)
     o = np.argsort(Nv, kind="stable")
     return dict(x0=x0[o], s_target=st[o], is_final=fin[o], N=Nv[o])
