@@ -8,7 +8,7 @@ bash tools/gpu_configs.sh || exit 1
 for c in ${PMC_CFGS:-C2}; do
   cd /tmp && export TMPDIR=/tmp
   rm -rf $R/gpurun_out/stats_$c
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/stats_$c -o run --output-format csv -- python3 $R/bench.py --config $c --steps 20 --warmup 3 --no-cpu --inflight 0 --nlp-steps 0 --closed-loop 0 > $R/gpurun_out/stats_$c.log 2>&1 || { echo "stats $c failed"; tail $R/gpurun_out/stats_$c.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/stats_$c -o run --output-format csv -- python3 $R/bench.py --config $c --steps 20 --warmup 3 --no-cpu --inflight 0 --nlp-steps 0 --closed-loop 0 --plan-chunks 0 > $R/gpurun_out/stats_$c.log 2>&1 || { echo "stats $c failed"; tail $R/gpurun_out/stats_$c.log; exit 1; }
   cd $R
   CFG=$c bash tools/gpu_f64_pmc.sh > /dev/null || { echo "f64 pmc $c failed"; exit 1; }
   python3 tools/pmc_f64.py $c $(find gpurun_out/stats_$c -name "*kernel_stats.csv" | head -1)
