@@ -112,12 +112,16 @@ int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, cons
 /* Same, with device pointers, launched asynchronously on `stream` (a hipStream_t; 0 = null stream).
  * On a host context (device = -1) the pointers are host memory and the call is synchronous.
  * Same argument contract as mpc_solve_batch (n_obs NULL = all max_obs rows; obs with max_obs == 0 is
- * MPC_E_ARG); u0 and U must be 16-byte aligned (they are written with 16-byte stores).  No host synchronisation and, once warmed up, no allocation (graph-capturable): the
+ * MPC_E_ARG); the double arrays must be 8-byte aligned (MPC_E_ARG otherwise); u0 and U are written
+ * with 16-byte stores when both are 16-byte aligned, else with 8-byte ones.  No host synchronisation and,
+ * once warmed up, no allocation (graph-capturable): the
  * two-phase work list is allocated by mpc_create for up to 2^20 instances (a larger B runs the
  * single-kernel path, same results).  With MPC_STAGE_CACHE=1 in the environment (off by default) the
  * two-phase launch also keeps the deferred instances' linearisation point and rollout (7N+5 doubles
  * each) in a cache that grows on the first eager call with a larger B (hipMalloc, which waits for the
- * device); a captured call that finds it too small runs without it (same results).  The work list belongs to the context: consecutive eager calls on one context are ordered
+ * device); a captured call never uses it (a later eager call may grow it, which would leave the graph
+ * with a freed pointer), same results.  The work list belongs to the context: consecutive eager calls on
+ * one context are ordered
  * on the device even when they use different streams (a call on a new stream waits for the previous
  * call's kernels), so their results never depend on the streams chosen.  A call made while `stream` is
  * being captured into a HIP graph records no such ordering (it would tie the graph to work outside

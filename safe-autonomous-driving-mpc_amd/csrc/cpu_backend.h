@@ -902,20 +902,33 @@ struct Backend {
     void parallel(const mpc_params& p, int n, Body body) const {
         const int nt = std::max(1, std::min(threads, (n + 7) / 8));
         std::atomic<int> next(0);
+        // a worker that cannot get its scratch leaves its share to the others; no exception leaves a thread
         auto run = [&]() {
-            std::unique_ptr<Worker> w(new Worker(*ref, p));
+            std::unique_ptr<Worker> w;
+            try {
+                w.reset(new Worker(*ref, p));
+            } catch (...) {
+                return;
+            }
             for (;;) {
                 const int i0 = next.fetch_add(8);
                 if (i0 >= n) break;
                 for (int i = i0; i < std::min(n, i0 + 8); ++i) body(*w, i);
             }
         };
-        if (nt == 1) { run(); return; }
         std::vector<std::thread> pool;
-        pool.reserve(nt - 1);
-        for (int t = 1; t < nt; ++t) pool.emplace_back(run);
+        if (nt > 1) {
+            try {
+                pool.reserve(nt - 1);
+                for (int t = 1; t < nt; ++t) pool.emplace_back(run);
+            } catch (...) {
+                // fewer threads than asked: the ones that started and this one finish the work
+            }
+        }
         run();
         for (auto& th : pool) th.join();
+        // every worker failed to start: nothing was solved
+        if (next.load() < n) throw std::bad_alloc();
     }
 
     // mpc_solve_batch on host buffers (the device entry's argument contract)

@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -1938,13 +1940,30 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int i = gl; i < 5 * NP; i += GL) o[2 * N + i] = S.Xr[i];
         }
     } else if (bvalid) {
-        // one 16-B store per lane (full cache lines, not two half-filled strided stores)
-        if (gl < N && Ug)
-            *reinterpret_cast<double2*>(Ug + (size_t)b * 2 * N + 2 * gl) = make_double2(S.ub[2 * gl], S.ub[2 * gl + 1]);
+        // one 16-B store per lane (full cache lines, not two half-filled strided stores) when the caller's
+        // buffers allow it; 8-B aligned views (e.g. a tensor slice at an odd offset) take two 8-B stores
+        const bool a16 = ((((uintptr_t)Ug) | ((uintptr_t)u0g)) & 15) == 0;
+        if (gl < N && Ug) {
+            double* o = Ug + (size_t)b * 2 * N + 2 * gl;
+            if (a16) {
+                *reinterpret_cast<double2*>(o) = make_double2(S.ub[2 * gl], S.ub[2 * gl + 1]);
+            } else {
+                o[0] = S.ub[2 * gl];
+                o[1] = S.ub[2 * gl + 1];
+            }
+        }
         if (Xg)
             for (int i = gl; i < 5 * NP; i += GL) Xg[(size_t)b * 5 * NP + i] = S.Xr[i];
         if (gl == 0) {
-            if (u0g) *reinterpret_cast<double2*>(u0g + 2 * (size_t)b) = make_double2(S.ub[0], S.ub[1]);
+            if (u0g) {
+                double* o = u0g + 2 * (size_t)b;
+                if (a16) {
+                    *reinterpret_cast<double2*>(o) = make_double2(S.ub[0], S.ub[1]);
+                } else {
+                    o[0] = S.ub[0];
+                    o[1] = S.ub[1];
+                }
+            }
             if (statusg) statusg[b] = status;
             if (itersg) itersg[b] = total_it;
         }
@@ -2139,6 +2158,24 @@ __global__ void mpc_pose_kernel(DevTable tab, int n, const double* __restrict__ 
 // host side: C ABI
 // ------------------------------------------------------------------------------------------
 static thread_local std::string g_err = "";
+
+static int fail(int code, const std::string& msg);
+
+// a host-backend call behind an extern "C" entry: no C++ exception crosses the ABI (worker threads that
+// cannot start, or allocations that fail, become MPC_E_ALLOC)
+template <typename F>
+static int host_call(F&& f) {
+    try {
+        f();
+        return MPC_SUCCESS;
+    } catch (const std::bad_alloc&) {
+        return fail(MPC_E_ALLOC, "host backend: out of memory");
+    } catch (const std::exception& e) {
+        return fail(MPC_E_ALLOC, std::string("host backend: ") + e.what());
+    } catch (...) {
+        return fail(MPC_E_ALLOC, "host backend: unexpected exception");
+    }
+}
 
 static int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -2451,7 +2488,9 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
             if (hipMalloc(&c->stc, need * sizeof(double)) == hipSuccess) c->cap_stc = need;
             else { c->stc = nullptr; (void)hipGetLastError(); }
         }
-        if (c->use_stc && need <= c->cap_stc) stc = c->stc;
+        // a captured call runs without the stage cache: a later eager call may grow (free and reallocate) it,
+        // and a graph holding the old pointer would then replay into freed memory
+        if (c->use_stc && need <= c->cap_stc && !capturing) stc = c->stc;
         if (capturing || c->wl_memset) {
             // a captured call resets its own count by a memset inside the graph, so every replay starts
             // from zero (an eager call's reset would not be replayed)
@@ -2517,13 +2556,12 @@ extern "C" int mpc_solve_batch_device(mpc_ctx* c, int B, const double* x0, const
         return fail(MPC_E_ARG, "obs given but params.max_obs == 0 (the obstacles would be ignored)");
     int rc = check_params(&c->p);
     if (rc) return rc;
+    if (((uintptr_t)u0 | (uintptr_t)U | (uintptr_t)x0 | (uintptr_t)Xpred | (uintptr_t)obs | (uintptr_t)ubar) & 7)
+        return fail(MPC_E_ARG, "double arrays must be 8-byte aligned");
     if (c->cpu) {
         // host context: the pointers are host memory and the call is synchronous (stream ignored)
-        c->cpu->solve_batch(c->p, B, x0, obs, n_obs, ubar, u0, U, Xpred, status, iters);
-        return MPC_SUCCESS;
+        return host_call([&] { c->cpu->solve_batch(c->p, B, x0, obs, n_obs, ubar, u0, U, Xpred, status, iters); });
     }
-    if (((uintptr_t)u0 | (uintptr_t)U) & 15)
-        return fail(MPC_E_ARG, "u0 and U must be 16-byte aligned (hipMalloc and torch allocations are)");
     KParams kp = kparams(&c->p);
     if (!obs) kp.max_obs = 0;
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
@@ -2548,10 +2586,10 @@ extern "C" int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double
     if (rc) return rc;
     const int N = c->p.N, mo = c->p.max_obs;
     if (obs && mo == 0) return fail(MPC_E_ARG, "obs given but params.max_obs == 0 (the obstacles would be ignored)");
-    if (c->cpu) {
-        c->cpu->solve_batch(c->p, B, x0, mo > 0 ? obs : nullptr, n_obs, ubar, u0, U, Xpred, status, iters);
-        return MPC_SUCCESS;
-    }
+    if (c->cpu)
+        return host_call([&] {
+            c->cpu->solve_batch(c->p, B, x0, mo > 0 ? obs : nullptr, n_obs, ubar, u0, U, Xpred, status, iters);
+        });
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);
     if ((size_t)B > c->cap_B || N > c->cap_N || mo > c->cap_obs) {
         size_t nb = (size_t)B > c->cap_B ? (size_t)B : c->cap_B;
@@ -2611,9 +2649,14 @@ extern "C" int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mp
     mpc_fsm F;
     if (fsm) F = *fsm; else mpc_default_fsm(&F);     // NULL: both scenarios off
     const bool with_fsm = fsm && (F.dynamic_obstacle || F.traffic_light);
-    if (c->cpu)
-        return c->cpu->closed_loop(c->p, B, x_init, F, with_fsm, max_steps, s_stop, hist_x, hist_u, hist_obs_s,
-                                   hist_tl, hist_status, n_steps, step_ms);
+    if (c->cpu) {
+        int hrc = MPC_SUCCESS;
+        const int erc = host_call([&] {
+            hrc = c->cpu->closed_loop(c->p, B, x_init, F, with_fsm, max_steps, s_stop, hist_x, hist_u, hist_obs_s,
+                                      hist_tl, hist_status, n_steps, step_ms);
+        });
+        return erc != MPC_SUCCESS ? erc : hrc;
+    }
     KParams kp = kparams(&c->p);
     kp.max_obs = with_fsm ? 2 : 0;          // the FSM yields at most the car and the light
     HIPCHK(hipSetDevice(c->device), MPC_E_DEVICE);

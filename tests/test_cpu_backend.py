@@ -100,6 +100,30 @@ def test_device_entry_on_host_context(env):
     assert np.array_equal(U, ref["U"]) and np.array_equal(X, ref["Xpred"]) and np.array_equal(st, ref["status"])
 
 
+def test_device_entry_alignment_contract(env):
+    """the device entry's contract is 8-byte aligned double arrays.  A pointer off by 4 bytes is
+    MPC_E_ARG with a message (on every context); 8-byte aligned views that are not 16-byte aligned (a slice
+    at an odd element offset) are accepted and give the aligned call's results (the GPU kernel falls back
+    to 8-byte stores for u0 / U; tests/test_gpu_device_entry.py checks that path)."""
+    mpcqp, _, _, W, _, _ = env
+    w = W.make_batch("C2", B=16)
+    ld = W.loader(w["traj"])
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=20), device=-1)
+    B = 16
+    x0 = np.ascontiguousarray(w["x0"])
+    st = np.zeros(B, np.int32); it = np.zeros(B, np.int32)
+    a = lambda v: v.ctypes.data
+    raw = np.zeros(2 * B * 20 * 8 + 64, np.uint8)
+    with pytest.raises(mpcqp.MpcError, match="8-byte aligned"):
+        slv.solve_batch_device(B, a(x0), None, None, None, None, a(raw) + 4, None, a(st), a(it), 0)
+    ref = slv.solve_batch(x0)
+    u0b = np.zeros(2 * B + 1); Ub = np.zeros(2 * B * 20 + 1); X = np.zeros((B, 21, 5))
+    u0, U = u0b[1:].reshape(B, 2), Ub[1:].reshape(B, 20, 2)
+    assert (u0.ctypes.data % 16, U.ctypes.data % 16) == (8, 8)
+    slv.solve_batch_device(B, a(x0), None, None, None, u0.ctypes.data, U.ctypes.data, a(X), a(st), a(it), 0)
+    assert np.array_equal(U, ref["U"]) and np.array_equal(u0, ref["u0"]) and np.array_equal(X, ref["Xpred"])
+
+
 def _host_loop(TT, mpc, fsm, traj, x0, max_steps):
     """The shim's run_simulation body from a given start (the solver is the context's: here the host one)."""
     x = np.asarray(x0, np.float64)

@@ -180,3 +180,68 @@ def test_graph_capture_on_side_stream_after_eager_warmup(lib):
     # an eager call after the replays (same stream) still orders correctly
     o2, _ = device_solve(slv, wa, torch)
     assert_identical(to_host(o2, torch), ra, "eager after graph")
+
+
+def test_device_entry_unaligned_outputs(lib):
+    """u0 and U that are 8-byte but not 16-byte aligned (tensor views at an odd element offset) take the
+    kernel's 8-byte store path and give the aligned call's results bit for bit."""
+    import torch
+    import workloads as W
+    wb = W.make_batch("C2", B=512)
+    slv = make_solver(lib, wb["traj"], wb["N"], 0)
+    out, _ = device_solve(slv, wb, torch)
+    ref = to_host(out, torch)
+    dev = torch.device("cuda", 0)
+    B, N = 512, wb["N"]
+    x0 = torch.as_tensor(wb["x0"], dtype=torch.float64, device=dev).contiguous()
+    u0b = torch.empty(2 * B + 1, dtype=torch.float64, device=dev)
+    Ub = torch.empty(2 * B * N + 1, dtype=torch.float64, device=dev)
+    u0, U = u0b[1:], Ub[1:]
+    assert u0.data_ptr() % 16 == 8 and U.data_ptr() % 16 == 8
+    X = torch.empty((B, N + 1, 5), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    slv.solve_batch_device(B, x0.data_ptr(), 0, 0, 0, u0.data_ptr(), U.data_ptr(), X.data_ptr(), st.data_ptr(),
+                           it.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(U.cpu().numpy().reshape(B, N, 2), ref["U"])
+    assert np.array_equal(u0.cpu().numpy().reshape(B, 2), ref["u0"])
+    assert np.array_equal(X.cpu().numpy(), ref["Xpred"]) and np.array_equal(st.cpu().numpy(), ref["status"])
+
+
+def test_stage_cache_capture_then_grow(lib):
+    """with MPC_STAGE_CACHE=1, a graph captured at B = 1024, then an eager call at B = 4096 that
+    grows (frees and reallocates) the context's stage cache, then replays of the graph: the captured call
+    never used the cache, so the replays stay correct."""
+    torch = pytest.importorskip("torch")
+    import workloads as W
+    old = os.environ.get("MPC_STAGE_CACHE")
+    os.environ["MPC_STAGE_CACHE"] = "1"
+    try:
+        wa = W.make_batch("C2", B=1024, seed=41)
+        slv = make_solver(lib, wa["traj"], wa["N"], 0)
+    finally:
+        if old is None:
+            del os.environ["MPC_STAGE_CACHE"]
+        else:
+            os.environ["MPC_STAGE_CACHE"] = old
+    ra = slv.solve_batch(wa["x0"])
+    out, keep = device_solve(slv, wa, torch)                     # eager warm-up at B = 1024
+    assert_identical(to_host(out, torch), ra, "eager")
+    x0 = keep[0]
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=side):
+        slv.solve_batch_device(1024, x0.data_ptr(), 0, 0, 0, out["u0"].data_ptr(), out["U"].data_ptr(),
+                               out["Xpred"].data_ptr(), out["status"].data_ptr(), out["iters"].data_ptr(),
+                               stream=torch.cuda.current_stream().cuda_stream)
+    wbig = W.make_batch("C2", B=4096, seed=42)
+    rbig = slv.solve_batch(wbig["x0"])
+    obig, _ = device_solve(slv, wbig, torch)                     # grows the stage cache
+    assert_identical(to_host(obig, torch), rbig, "eager after growth")
+    for _ in range(2):
+        for k in out:
+            out[k].zero_()
+        g.replay()
+        assert_identical(to_host(out, torch), ra, "replay after growth")
