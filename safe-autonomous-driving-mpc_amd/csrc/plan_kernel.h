@@ -418,32 +418,35 @@ __device__ bool solve5(double M[25], double R[5 * NC]) {
     return true;
 }
 
-// L L' = H (3 x 3) with the diagonal of L stored inverted (L[0] = 1/l00, L[2] = 1/l11, L[5] = 1/l22), so
-// the solves multiply instead of divide: 3 divisions per factorisation instead of 6 per solve, which sit on
-// the solves' dependent chains (oracle/plan_oracle.c uses the same form and rounding)
+// H (3 x 3, symmetric positive definite) = L D L' with L unit lower triangular, stored as {1/d0, l10, 1/d1,
+// l20, l21, 1/d2}: no square roots, three divisions per factorisation and none in the solves, which sit on
+// the solves' dependent chains (oracle/plan_oracle.c uses the same form and rounding).  Fails (false) when a
+// pivot is not positive, the Cholesky condition.
 __device__ bool chol3(const double H[3][3], double L[6]) {
-    if (!(H[0][0] > 0.0)) return false;
-    L[0] = 1.0 / sqrt(H[0][0]);
+    const double d0 = H[0][0];
+    if (!(d0 > 0.0)) return false;
+    L[0] = 1.0 / d0;
     L[1] = H[1][0] * L[0];
-    const double d1 = H[1][1] - L[1] * L[1];
+    const double d1 = H[1][1] - L[1] * H[1][0];
     if (!(d1 > 0.0)) return false;
-    L[2] = 1.0 / sqrt(d1);
+    L[2] = 1.0 / d1;
     L[3] = H[2][0] * L[0];
-    L[4] = (H[2][1] - L[3] * L[1]) * L[2];
-    const double d2 = H[2][2] - L[3] * L[3] - L[4] * L[4];
+    const double e21 = H[2][1] - L[3] * H[1][0];
+    L[4] = e21 * L[2];
+    const double d2 = H[2][2] - L[3] * H[2][0] - L[4] * e21;
     if (!(d2 > 0.0)) return false;
-    L[5] = 1.0 / sqrt(d2);
+    L[5] = 1.0 / d2;
     return true;
 }
 
-// b <- (L L')^-1 b
+// b <- (L D L')^-1 b
 __device__ inline void chol3_solve(const double L[6], double b[3]) {
-    const double y0 = b[0] * L[0];
-    const double y1 = (b[1] - L[1] * y0) * L[2];
-    const double y2 = (b[2] - L[3] * y0 - L[4] * y1) * L[5];
+    const double y0 = b[0];
+    const double y1 = b[1] - L[1] * y0;
+    const double y2 = b[2] - L[3] * y0 - L[4] * y1;
     b[2] = y2 * L[5];
-    b[1] = (y1 - L[4] * b[2]) * L[2];
-    b[0] = (y0 - L[1] * b[1] - L[3] * b[2]) * L[0];
+    b[1] = y1 * L[2] - L[4] * b[2];
+    b[0] = y0 * L[0] - L[1] * b[1] - L[3] * b[2];
 }
 
 __host__ __device__ constexpr int hx(int i, int j) {   // packed index of the symmetric 8x8 (i <= j)
