@@ -126,3 +126,25 @@ def test_full_trajectory_on_gpu_passes_reference_check(env, capsys):
               f"{'passed' if q['passed'] else 'FAILED'}")
         assert "===> Checks passed : True" in out, out
         assert q["passed"] and np.isin(st, (0, 4)).mean() >= 0.9
+
+
+@pytest.mark.parametrize("N", [1, 2, 48, 64])
+def test_horizon_extremes_vs_oracle(env, N):
+    """The smallest horizons and the largest (PLAN_MAX_N = 64: ~155 KB of LDS per chunk, above the 64 KB
+    default, which plan_solve_chunks_device raises with hipFuncSetAttribute): statuses and, on chunks both
+    call converged, plans equal to the oracle's within 1e-8."""
+    mpcplan, PO, W = env
+    r = W.plan_route("synth2")
+    wb = W.plan_batch(r, N, 24, seed=100 + N, final_frac=0.25)
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=N))
+    g = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    pl.close()
+    o = PO.PlanOracle(r).solve_batch(PO.default_params(N=N), wb["x0"], wb["s_target"], wb["is_final"], num_threads=16)
+    agree = float((g["status"] == o["status"]).mean())
+    both = np.isin(g["status"], (0, 4)) & np.isin(o["status"], (0, 4))
+    err = max((float(np.abs(g[k][both] - o[k][both]).max()) for k in ("X", "U", "S")), default=0.0) if both.any() else 0.0
+    print(f"N={N}: status agree {agree:.3f}, both converged {int(both.sum())}/24, max err {err:.1e}, "
+          f"GPU statuses {np.bincount(g['status'], minlength=5).tolist()}")
+    assert agree >= 0.9
+    assert err <= TOL
+    assert np.isfinite(g["X"]).all()
