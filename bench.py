@@ -564,6 +564,10 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
                "status_names": [mpcplan.STATUS_NAMES[i] for i in range(5)],
                "sqp_mean": float(sqp.mean()), "qp_ipm_iters_mean": float(iters.mean()),
                "launches_per_step": len(groups), "streams": len(side),
+               "roofline": dict(executed_work("plan"), bound="fp64-valu", peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
+                                note="the chunk kernel is latency-bound (one wave per SIMD, sequential Riccati "
+                                     "recursions, DESIGN.md 5c); executed FP64 from its PMC pass over N = 16, "
+                                     "16384 chunks (tools/gpu_plan_pmc.sh)"),
                "note": "HIP events on the timing stream, which joins the side streams that run one launch per "
                        "horizon; inputs resident in HBM"}
         if with_cpu:

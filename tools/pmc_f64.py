@@ -10,7 +10,8 @@ Per launch of each kernel (mode XO / IPM / FULL / ONE, template <OBS, G, MODE, N
 With a kernel-stats CSV (rocprofv3 --stats, same config) the flops are divided by the kernel's average
 duration to give executed TFLOP/s and its fraction of the 78.6 TF FP64 peak.
 
-  python tools/pmc_f64.py C2 [stats.csv]   ->  gpurun_out/pmc_f64.csv and one JSON line
+  python tools/pmc_f64.py C2 [stats.csv]   ->  gpurun_out/pmc_f64_C2.csv and one JSON line per kernel
+  python tools/pmc_f64.py plan [stats.csv] ->  the planner kernel (tools/gpu_plan_pmc.sh)
 """
 import csv
 import glob
@@ -26,6 +27,8 @@ CTRS = ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64
 
 
 def kernel_key(name):
+    if "plan_chunk_kernel" in name:
+        return "plan_chunk_kernel"
     if "mpc_solve_kernel" not in name:
         return None
     try:
