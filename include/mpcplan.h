@@ -92,8 +92,10 @@ int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const 
                       int* sqp);
 
 /* Same with device pointers, asynchronous on `stream` (hipStream_t; NULL = the null stream).  Nmax must
- * bound every N[b] (N NULL: params N).  Scratch is owned by the context (grown on demand, never while a
- * graph capture is active on the stream: then a call that needs more scratch fails with PLAN_E_ALLOC). */
+ * bound every N[b] (N NULL: params N); a chunk whose N[b] lies outside [1, Nmax] is not solved (zero plan,
+ * status PLAN_NUMERICAL).  The kernel needs no scratch memory: each chunk's working set lives in LDS
+ * (about 2.4 KB per stage, sized for Nmax; Nmax is limited by the device's LDS per workgroup, 64 at 160 KB),
+ * so the call allocates nothing and can be captured into a graph. */
 int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const double* x0,
                              const double* s_target, const int* is_final, double* X, double* U, double* S,
                              int* status, int* iters, int* sqp, void* stream);

@@ -1588,6 +1588,24 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
     X.ln = threadIdx.x;
     X.dbg = a.dbg;
     X.N = a.N ? a.N[b] : a.Nfixed;
+    if (X.N < 1 || X.N > a.Nmax) {
+        // a per-chunk horizon outside [1, Nmax] (device arrays are not validated on the host): no solve, zero
+        // plan, status PLAN_NUMERICAL (the chunk's LDS block is sized for Nmax)
+        for (int k = threadIdx.x; k <= a.Nmax; k += WAVE) {
+            if (a.X)
+                for (int i = 0; i < 5; ++i) a.X[((size_t)b * (a.Nmax + 1) + k) * 5 + i] = 0.0;
+            if (k < a.Nmax) {
+                if (a.U) a.U[((size_t)b * a.Nmax + k) * 2] = a.U[((size_t)b * a.Nmax + k) * 2 + 1] = 0.0;
+                if (a.S) a.S[(size_t)b * a.Nmax + k] = 0.0;
+            }
+        }
+        if (threadIdx.x == 0) {
+            if (a.status) a.status[b] = PLAN_NUMERICAL;
+            if (a.iters) a.iters[b] = 0;
+            if (a.sqp) a.sqp[b] = 0;
+        }
+        return;
+    }
     const int N = X.N;
     X.fin = a.fin ? (a.fin[b] != 0) : 0;
 #pragma unroll

@@ -148,3 +148,29 @@ def test_horizon_extremes_vs_oracle(env, N):
     assert agree >= 0.9
     assert err <= TOL
     assert np.isfinite(g["X"]).all()
+
+
+def test_device_horizon_out_of_range_is_flagged(env):
+    """Per-chunk horizons come from device memory unchecked by the host: a chunk with N[b] = 0 or N[b] > Nmax
+    is not solved (zero plan, PLAN_NUMERICAL) and its neighbours are unaffected."""
+    import torch
+    mpcplan, PO, W = env
+    r = W.plan_route("synth1")
+    wb = W.plan_batch(r, 12, 6, seed=5)
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=12))
+    h = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    Nv = t(np.array([12, 0, 12, 13, 12, -3], np.int32), torch.int32)
+    x0, st, fin = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32)
+    X = torch.full((6, 13, 5), 7.0, dtype=torch.float64, device=dev)
+    o = [torch.full((6,), -1, dtype=torch.int32, device=dev) for _ in range(3)]
+    pl.solve_chunks_device(6, 12, Nv.data_ptr(), x0.data_ptr(), st.data_ptr(), fin.data_ptr(), X.data_ptr(), 0, 0,
+                           *[a.data_ptr() for a in o], stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    Xh, sth = X.cpu().numpy(), o[0].cpu().numpy()
+    for b in (1, 3, 5):
+        assert sth[b] == mpcplan.PLAN_NUMERICAL and (Xh[b] == 0).all()
+    for b in (0, 2, 4):
+        assert sth[b] == h["status"][b] and np.array_equal(Xh[b], h["X"][b])
+    pl.close()
