@@ -517,22 +517,30 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
     order = sorted(range(len(groups)), key=lambda g: -groups[g][0])
     d8, d4 = 8, 4
 
-    def step():
-        e0 = torch.cuda.Event()
-        e0.record(stream)
+    def launches():
         for k, g in enumerate(order):
             n, i0, i1, Xg, Ug, Sg = groups[g]
-            ss = side[k % len(side)]
-            if k < len(side):
-                ss.wait_event(e0)
             pl.solve_chunks_device(i1 - i0, n, Nd.data_ptr() + d4 * i0, x0.data_ptr() + d8 * 5 * i0,
                                    st.data_ptr() + d8 * i0, fin.data_ptr() + d4 * i0, Xg.data_ptr(), Ug.data_ptr(),
                                    Sg.data_ptr(), o[0].data_ptr() + d4 * i0, o[1].data_ptr() + d4 * i0,
-                                   o[2].data_ptr() + d4 * i0, stream=ss.cuda_stream)
+                                   o[2].data_ptr() + d4 * i0, stream=side[k % len(side)].cuda_stream)
+
+    def fork():
+        e0 = torch.cuda.Event()
+        e0.record(stream)
+        for ss in side:
+            ss.wait_event(e0)
+
+    def join():
         for ss in side:
             e = torch.cuda.Event()
             e.record(ss)
             stream.wait_event(e)
+
+    def step():
+        fork()
+        launches()
+        join()
     step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -551,6 +559,24 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    # secondary: the same batches back to back with no join between them (a planning service fed
+    # continuously), so one batch's slowest chunks overlap the next batch's launches on the other streams
+    if world > 1:
+        dist.barrier()
+    ep = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    t1 = time.perf_counter()
+    ep[0].record(stream)
+    fork()
+    for i in range(steps):
+        launches()
+    join()
+    ep[1].record(stream)
+    torch.cuda.synchronize(dev)
+    pel = max(time.perf_counter() - t1, ep[0].elapsed_time(ep[1]) / 1e3)
+    if world > 1:
+        tt = torch.tensor([pel], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        pel = float(tt.item())
     status, iters, sqp = (a.cpu().numpy() for a in o)
     out = None
     if rank == 0:
@@ -564,6 +590,9 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
                "status_names": [mpcplan.STATUS_NAMES[i] for i in range(5)],
                "sqp_mean": float(sqp.mean()), "qp_ipm_iters_mean": float(iters.mean()),
                "launches_per_step": len(groups), "streams": len(side),
+               "pipelined": {"value": world * Bl * steps / pel, "unit": "chunks/s", "batches": steps,
+                             "note": "the same batches back to back without a join between them (a continuously "
+                                     "fed planning service); secondary, value is one batch at a time"},
                "roofline": dict(executed_work("plan"), bound="fp64-valu", peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
                                 note="the chunk kernel is latency-bound (one wave per SIMD, sequential Riccati "
                                      "recursions, DESIGN.md 5c); executed FP64 from its PMC pass over N = 16, "
