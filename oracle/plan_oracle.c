@@ -48,6 +48,7 @@
 #define NZMAX (5 * (PLAN_MAX_N + 1) + 3 * PLAN_MAX_N)
 #define RHO 1e8               /* penalty of the active rows in the equality-constrained solve */
 #define AL_STEPS 4            /* refinement + multiplier updates of that solve */
+#define AL_TOL 1e-13        /* stop the refinements once the multiplier update is at rounding level */
 #define POLISH_ROUNDS 6
 #define SHIFT0 1.0            /* interior-point start: s = max(row, 0) + SHIFT0, lambda = 1 */
 #define TAU 0.995
@@ -869,9 +870,17 @@ static int eqp(qp_t* Q, unsigned char act[][NR], double z[][NZ], double lam[][NR
         solve(Q, &F, (const double(*)[NZ])gl, rE, dz, nu);
         for (int k = 0; k <= N; ++k)
             for (int u = 0; u < NZ; ++u) z[k][u] += dz[k][u];
+        double upd = 0.0, ym = 0.0;
         for (int k = 0; k <= N; ++k)
             for (int j = 0; j < Q->nr[k]; ++j)
-                if (act[k][j]) y[k][j] -= RHO * row_val(Q, k, j, z[k]);
+                if (act[k][j]) {
+                    const double d = RHO * row_val(Q, k, j, z[k]);
+                    y[k][j] -= d;
+                    upd = fmax(upd, fabs(d));
+                    ym = fmax(ym, fabs(y[k][j]));
+                }
+        /* the multiplier update has reached rounding level: further refinements change nothing */
+        if (upd <= AL_TOL * (1.0 + ym)) break;
     }
     if (!finite_z(Q, (const double(*)[NZ])z)) return -1;
     int bad = 0;

@@ -25,6 +25,7 @@ constexpr int NR = 11;            // rows per stage at most
 constexpr int NH = 36;            // packed symmetric 8x8
 constexpr double RHO = 1e8;       // penalty of the active rows in the equality-constrained solve
 constexpr int AL_STEPS = 4;
+constexpr double AL_TOL = 1e-13;   // refinements stop once the multiplier update is at rounding level
 constexpr int POLISH_ROUNDS = 6;
 constexpr double SHIFT0 = 1.0;
 constexpr double TAU = 0.995;
@@ -1165,6 +1166,7 @@ __device__ int eqp(Ctx& X, double scale) {
         sync();
         const double rE[2] = {X.e[0] - L[Y.oTZ + NZ * N + 0], X.e[1] - L[Y.oTZ + NZ * N + 4]};
         solve(X, rE);
+        double upd = 0.0, ym = 0.0;
         for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oTZ + NZ * k + u] += L[Y.oDZ + NZ * k + u];
@@ -1174,11 +1176,20 @@ __device__ int eqp(Ctx& X, double scale) {
             const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
             const unsigned act = (unsigned)L[Y.oTACT + k];
             for_rows(k, N, X.fin, [&](int kind, int j) {
-                if ((act >> j) & 1u)
-                    L[Y.oY + NR * k + j] -= RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
+                if ((act >> j) & 1u) {
+                    const double d = RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
+                    const double y = L[Y.oY + NR * k + j] - d;
+                    L[Y.oY + NR * k + j] = y;
+                    upd = fmax(upd, fabs(d));
+                    ym = fmax(ym, fabs(y));
+                }
             });
         }
+        upd = wmax(upd);
+        ym = wmax(ym);
         sync();
+        // the multiplier update has reached rounding level: further refinements change nothing
+        if (upd <= AL_TOL * (1.0 + ym)) break;
     }
     double fin = 1.0;
     int bad = 0;
