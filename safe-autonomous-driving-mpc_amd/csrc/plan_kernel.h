@@ -69,7 +69,7 @@ inline void route_grid(const double* s, int M, int T, int* grid, double* ginv) {
 // point alias the polish's: DSA = Y, DLA = TLAM, DS = TZ (the polish runs after the interior point is done).
 struct Layout {
     int NP;
-    int oA, oB, oC, oH, oHT, oGQ, oG, oK, oL, oEZ, oZ, oS, oLAM, oGL, oDZ, oDSA, oDLA, oDS, oDL, oMY, oMLAT, oZB,
+    int oA, oB, oC, oH, oHS, oGQ, oG, oK, oL, oEZ, oZ, oS, oLAM, oGL, oDZ, oDSA, oDLA, oDS, oDL, oMY, oMLAT, oZB,
         oZ2, oDZV, oPI, oVLIM, oVL, oACT, oTACT, oSC, oWK;
     int oY, oTLAM, oTZ;
     int total;
@@ -84,7 +84,8 @@ __host__ __device__ Layout make_layout(int Nmax) {
     y.oB = o; o += 10 * np;          // u1, u2 columns (the slack's column is zero)
     y.oC = o; o += 5 * np;
     y.oH = o; o += NH * np;
-    y.oHT = o; o += NH * np;         // H + delta I + row weights (the factorisation's stage Hessian)
+    y.oHS = o; o += 8 * np;          // the factorisation's stage Hessian H + delta I + row weights at the 8
+                                     // entries rows touch (hs_slot); elsewhere it is H + delta I
     y.oGQ = o; o += NZ * np;
     y.oG = o; o += NR * np;
     y.oK = o; o += 15 * np;
@@ -104,7 +105,6 @@ __host__ __device__ Layout make_layout(int Nmax) {
     y.oZB = o; o += NZ * np;
     y.oZ2 = o; o += NZ * np;
     y.oDZV = o; o += NZ * np;
-    y.oPI = o; o += 5 * np;
     y.oVLIM = o; o += np;
     y.oVL = o; o += np;
     y.oACT = o; o += np;             // active-row bit masks (11 bits), stored as doubles
@@ -117,6 +117,7 @@ __host__ __device__ Layout make_layout(int Nmax) {
     y.oY = y.oDSA;
     y.oTLAM = y.oDLA;
     y.oTZ = y.oDS;
+    y.oPI = y.oDZ;                   // co-states of the multiplier recovery (after the QP's last solve)
     y.total = o;
     return y;
 }
@@ -455,6 +456,14 @@ __host__ __device__ constexpr int hx(int i, int j) {   // packed index of the sy
 }
 __device__ inline int hidx(int i, int j) { return i <= j ? hx(i, j) : hx(j, i); }
 
+// the 8 entries of a stage Hessian the rows touch, slots 0..7: (0,0) terminal row; (3,3), (3,4), (4,4) curvature
+// and lateral rows; (4,7) and (7,7) speed and slack rows (with (4,4)); (5,5), (6,6) control boxes
+__device__ inline int hs_slot(int u, int w) {
+    const int a = u < w ? u : w, b = u < w ? w : u;
+    if (a == b) return a == 0 ? 0 : a == 3 ? 1 : a == 4 ? 3 : a == 5 ? 5 : a == 6 ? 6 : a == 7 ? 7 : -1;
+    return (a == 3 && b == 4) ? 2 : (a == 4 && b == 7) ? 4 : -1;
+}
+
 // ------------------------------------------------------------------------------------------------------
 // the chunk: LDS working set, per-lane view
 // ------------------------------------------------------------------------------------------------------
@@ -773,9 +782,19 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     for (int k = X.ln; k <= N; k += WAVE) {
+        // only the 8 entries rows touch are stored (hs_slot); the rest of the factorisation Hessian is
+        // H + delta I, formed where it is read (ht_at)
         double H[NH];
 #pragma unroll
-        for (int i = 0; i < NH; ++i) H[i] = L[Y.oH + NH * k + i];
+        for (int i = 0; i < NH; ++i) H[i] = 0.0;
+        H[hx(0, 0)] = L[Y.oH + NH * k + hx(0, 0)];
+        H[hx(3, 3)] = L[Y.oH + NH * k + hx(3, 3)];
+        H[hx(3, 4)] = L[Y.oH + NH * k + hx(3, 4)];
+        H[hx(4, 4)] = L[Y.oH + NH * k + hx(4, 4)];
+        H[hx(4, 7)] = L[Y.oH + NH * k + hx(4, 7)];
+        H[hx(5, 5)] = L[Y.oH + NH * k + hx(5, 5)];
+        H[hx(6, 6)] = L[Y.oH + NH * k + hx(6, 6)];
+        H[hx(7, 7)] = L[Y.oH + NH * k + hx(7, 7)];
         const int nv = k < N ? NZ : 5;
 #pragma unroll
         for (int i = 0; i < NZ; ++i)
@@ -792,8 +811,15 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
                 H[hx(r.i1, r.i1)] += w * r.c1 * r.c1;
             }
         });
-#pragma unroll
-        for (int i = 0; i < NH; ++i) L[Y.oHT + NH * k + i] = H[i];
+        ldsd* hs = L + Y.oHS + 8 * k;
+        hs[0] = H[hx(0, 0)];
+        hs[1] = H[hx(3, 3)];
+        hs[2] = H[hx(3, 4)];
+        hs[3] = H[hx(4, 4)];
+        hs[4] = H[hx(4, 7)];
+        hs[5] = H[hx(5, 5)];
+        hs[6] = H[hx(6, 6)];
+        hs[7] = H[hx(7, 7)];
     }
 }
 
@@ -941,6 +967,15 @@ __device__ inline double ab_at(const Ctx& X, int k, int l, int j) {
     return j < 5 ? X.L[X.Y.oA + 25 * k + 5 * l + j] : X.L[X.Y.oB + 10 * k + 2 * l + (j - 5)];
 }
 
+// entry (u, w) of stage k's factorisation Hessian: the stored value at the rows' entries, else H + delta I
+// (the same sums stage_hess_par forms)
+__device__ inline double ht_at(const Ctx& X, int k, int u, int w) {
+    const int sl = hs_slot(u, w);
+    if (sl >= 0) return X.L[X.Y.oHS + 8 * k + sl];
+    const double h = X.L[X.Y.oH + NH * k + hidx(u, w)];
+    return (u == w && u < (k < X.N ? NZ : 5)) ? h + X.delta : h;
+}
+
 // Riccati factorisation of the HT stage Hessians over the wave (uniform result: false when a control
 // pivot is not positive, or the final chunk's terminal system is singular).  Per stage, backwards:
 //   M = HT + [A B 0]' P [A B 0]  (xx, wx, ww)       49 lanes, one entry each (the column of P [A B] it
@@ -956,7 +991,7 @@ __device__ bool factor_par(const Ctx& X) {
     const Layout& Y = X.Y;
     ldsd* P = L + Y.oWK;
     ldsd* M = P + 25;
-    if (ln < 25) P[ln] = L[Y.oHT + NH * N + hidx(ln / 5, ln % 5)];
+    if (ln < 25) P[ln] = ht_at(X, N, ln / 5, ln % 5);
     sync();
     for (int k = N - 1; k >= 0; --k) {
         if (ln < 49) {
@@ -964,7 +999,7 @@ __device__ bool factor_par(const Ctx& X) {
             if (ln < 25) { u = ln / 5; w = ln % 5; }
             else if (ln < 40) { u = 5 + (ln - 25) / 5; w = (ln - 25) % 5; }
             else { u = 5 + (ln - 40) / 3; w = 5 + (ln - 40) % 3; }
-            double m = L[Y.oHT + NH * k + hidx(u, w)];
+            double m = ht_at(X, k, u, w);
             if (u < 7 && w < 7) {
                 double pab[5];                      // column w of P [A | B], formed in this lane
 #pragma unroll
