@@ -23,6 +23,11 @@ constexpr int WAVE = 64;
 constexpr int NZ = 8;             // stage variables: x (s, d, o, k, v), w (u1, u2, S)
 constexpr int NR = 11;            // rows per stage at most
 constexpr int NH = 36;            // packed symmetric 8x8
+// LDS strides of the per-stage 8-vectors and stage Hessians: one double of padding each, so the lanes of a
+// stage-parallel loop (lane k on stage k) spread over the LDS banks (a stride of 8 doubles = 16 dwords put
+// every fourth lane on the same bank group: SQ_LDS_BANK_CONFLICT was 39% of the LDS-active cycles)
+constexpr int ZS = NZ + 1;
+constexpr int HSTR = NH + 1;
 constexpr double RHO = 1e8;       // penalty of the active rows in the equality-constrained solve
 constexpr int AL_STEPS = 4;
 constexpr double AL_TOL = 1e-13;   // refinements stop once the multiplier update is at rounding level
@@ -83,28 +88,28 @@ __host__ __device__ Layout make_layout(int Nmax) {
     y.oA = o; o += 25 * np;
     y.oB = o; o += 10 * np;          // u1, u2 columns (the slack's column is zero)
     y.oC = o; o += 5 * np;
-    y.oH = o; o += NH * np;
+    y.oH = o; o += HSTR * np;
     y.oHS = o; o += 8 * np;          // the factorisation's stage Hessian H + delta I + row weights at the 8
                                      // entries rows touch (hs_slot); elsewhere it is H + delta I
-    y.oGQ = o; o += NZ * np;
+    y.oGQ = o; o += ZS * np;
     y.oG = o; o += NR * np;
     y.oK = o; o += 15 * np;
     y.oL = o; o += 6 * np;
-    y.oEZ = o; o += 2 * NZ * np;
-    y.oZ = o; o += NZ * np;
+    y.oEZ = o; o += 2 * ZS * np;
+    y.oZ = o; o += ZS * np;
     y.oS = o; o += NR * np;
     y.oLAM = o; o += NR * np;
-    y.oGL = o; o += NZ * np;
-    y.oDZ = o; o += NZ * np;
+    y.oGL = o; o += ZS * np;
+    y.oDZ = o; o += ZS * np;
     y.oDSA = o; o += NR * np;
     y.oDLA = o; o += NR * np;
     y.oDS = o; o += NR * np;
     y.oDL = o; o += NR * np;
     y.oMY = o; o += 5 * np;
     y.oMLAT = o; o += 2 * np;
-    y.oZB = o; o += NZ * np;
-    y.oZ2 = o; o += NZ * np;
-    y.oDZV = o; o += NZ * np;
+    y.oZB = o; o += ZS * np;
+    y.oZ2 = o; o += ZS * np;
+    y.oDZV = o; o += ZS * np;
     y.oVLIM = o; o += np;
     y.oVL = o; o += np;
     y.oACT = o; o += np;             // active-row bit masks (11 bits), stored as doubles
@@ -661,7 +666,7 @@ __device__ void interval_hess_fold(Ctx& X, int k, const double xa[5], const doub
             if (i < 5) v += HabT[i][j];
             if (j < 5) v += HabT[j][i];
             if (i < 5 && j < 5) v += Haa[5 * i + j];
-            L[Y.oH + NH * k + hx(i, j)] += v;
+            L[Y.oH + HSTR * k + hx(i, j)] += v;
         }
     double hbc[5];
 #pragma unroll
@@ -679,7 +684,7 @@ __device__ void interval_hess_fold(Ctx& X, int k, const double xa[5], const doub
         if (i < 5)
 #pragma unroll
             for (int m = 0; m < 5; ++m) v += Hab[5 * i + m] * c[m];
-        L[Y.oGQ + NZ * k + i] += v;
+        L[Y.oGQ + ZS * k + i] += v;
     }
 }
 
@@ -695,29 +700,29 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
     for (int k = X.ln; k <= N; k += WAVE) {
         double x[5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) x[i] = L[Y.oZB + NZ * k + i];
+        for (int i = 0; i < 5; ++i) x[i] = L[Y.oZB + ZS * k + i];
 #pragma unroll
-        for (int i = 0; i < NH; ++i) L[Y.oH + NH * k + i] = 0.0;
+        for (int i = 0; i < NH; ++i) L[Y.oH + HSTR * k + i] = 0.0;
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) L[Y.oGQ + NZ * k + i] = 0.0;
-        const double u1 = k < N ? L[Y.oZB + NZ * k + 5] : 0.0, u2 = k < N ? L[Y.oZB + NZ * k + 6] : 0.0;
-        const double sl = k < N ? L[Y.oZB + NZ * k + 7] : 0.0;
+        for (int i = 0; i < NZ; ++i) L[Y.oGQ + ZS * k + i] = 0.0;
+        const double u1 = k < N ? L[Y.oZB + ZS * k + 5] : 0.0, u2 = k < N ? L[Y.oZB + ZS * k + 6] : 0.0;
+        const double sl = k < N ? L[Y.oZB + ZS * k + 7] : 0.0;
         if (k < N) {
-            L[Y.oH + NH * k + hx(0, 0)] = 2.0 * P.w_s / (den * den);
-            L[Y.oH + NH * k + hx(1, 1)] = 2.0 * P.w_y;
-            L[Y.oH + NH * k + hx(2, 2)] = 2.0 * P.w_y;
-            L[Y.oH + NH * k + hx(5, 5)] = 2.0 * P.w_u;
-            L[Y.oH + NH * k + hx(6, 6)] = 2.0 * P.w_u;
-            L[Y.oH + NH * k + hx(7, 7)] = 2.0 * P.w_slack;
-            L[Y.oGQ + NZ * k + 0] = -2.0 * P.w_s * (X.R.s_total - x[0]) / (den * den);
-            L[Y.oGQ + NZ * k + 1] = 2.0 * P.w_y * x[1];
-            L[Y.oGQ + NZ * k + 2] = 2.0 * P.w_y * x[2];
-            L[Y.oGQ + NZ * k + 5] = 2.0 * P.w_u * u1;
-            L[Y.oGQ + NZ * k + 6] = 2.0 * P.w_u * u2;
-            L[Y.oGQ + NZ * k + 7] = 2.0 * P.w_slack * sl;
+            L[Y.oH + HSTR * k + hx(0, 0)] = 2.0 * P.w_s / (den * den);
+            L[Y.oH + HSTR * k + hx(1, 1)] = 2.0 * P.w_y;
+            L[Y.oH + HSTR * k + hx(2, 2)] = 2.0 * P.w_y;
+            L[Y.oH + HSTR * k + hx(5, 5)] = 2.0 * P.w_u;
+            L[Y.oH + HSTR * k + hx(6, 6)] = 2.0 * P.w_u;
+            L[Y.oH + HSTR * k + hx(7, 7)] = 2.0 * P.w_slack;
+            L[Y.oGQ + ZS * k + 0] = -2.0 * P.w_s * (X.R.s_total - x[0]) / (den * den);
+            L[Y.oGQ + ZS * k + 1] = 2.0 * P.w_y * x[1];
+            L[Y.oGQ + ZS * k + 2] = 2.0 * P.w_y * x[2];
+            L[Y.oGQ + ZS * k + 5] = 2.0 * P.w_u * u1;
+            L[Y.oGQ + ZS * k + 6] = 2.0 * P.w_u * u2;
+            L[Y.oGQ + ZS * k + 7] = 2.0 * P.w_slack * sl;
             double xb[5], D1[25], R[5 * 8];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) xb[i] = L[Y.oZB + NZ * (k + 1) + i];
+            for (int i = 0; i < 5; ++i) xb[i] = L[Y.oZB + ZS * (k + 1) + i];
             interval_jac(X, x, xb, u1, u2, D1, R);
             if (!solve5<8>(D1, R)) {
                 ok = false;
@@ -760,16 +765,16 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
         }
         if (exact && k > 0 && !(X.fin && k == N)) {
             const double lp = L[Y.oMLAT + 2 * k], lm = L[Y.oMLAT + 2 * k + 1];
-            L[Y.oH + NH * k + hx(3, 4)] += 2.0 * v * (lp - lm);
-            L[Y.oH + NH * k + hx(4, 4)] += 2.0 * kk * (lp - lm);
+            L[Y.oH + HSTR * k + hx(3, 4)] += 2.0 * v * (lp - lm);
+            L[Y.oH + HSTR * k + hx(4, 4)] += 2.0 * kk * (lp - lm);
         }
     }
     ok = wmin(ok ? 1.0 : 0.0) > 0.0;
     sync();
 #pragma unroll
     for (int i = 0; i < 5; ++i) X.xi0[i] = X.x0[i] - L[Y.oZB + i];
-    X.e[0] = X.st - L[Y.oZB + NZ * N + 0];
-    X.e[1] = -L[Y.oZB + NZ * N + 4];
+    X.e[0] = X.st - L[Y.oZB + ZS * N + 0];
+    X.e[1] = -L[Y.oZB + ZS * N + 4];
     X.delta = 0.0;
     return ok;
 }
@@ -787,19 +792,19 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
         double H[NH];
 #pragma unroll
         for (int i = 0; i < NH; ++i) H[i] = 0.0;
-        H[hx(0, 0)] = L[Y.oH + NH * k + hx(0, 0)];
-        H[hx(3, 3)] = L[Y.oH + NH * k + hx(3, 3)];
-        H[hx(3, 4)] = L[Y.oH + NH * k + hx(3, 4)];
-        H[hx(4, 4)] = L[Y.oH + NH * k + hx(4, 4)];
-        H[hx(4, 7)] = L[Y.oH + NH * k + hx(4, 7)];
-        H[hx(5, 5)] = L[Y.oH + NH * k + hx(5, 5)];
-        H[hx(6, 6)] = L[Y.oH + NH * k + hx(6, 6)];
-        H[hx(7, 7)] = L[Y.oH + NH * k + hx(7, 7)];
+        H[hx(0, 0)] = L[Y.oH + HSTR * k + hx(0, 0)];
+        H[hx(3, 3)] = L[Y.oH + HSTR * k + hx(3, 3)];
+        H[hx(3, 4)] = L[Y.oH + HSTR * k + hx(3, 4)];
+        H[hx(4, 4)] = L[Y.oH + HSTR * k + hx(4, 4)];
+        H[hx(4, 7)] = L[Y.oH + HSTR * k + hx(4, 7)];
+        H[hx(5, 5)] = L[Y.oH + HSTR * k + hx(5, 5)];
+        H[hx(6, 6)] = L[Y.oH + HSTR * k + hx(6, 6)];
+        H[hx(7, 7)] = L[Y.oH + HSTR * k + hx(7, 7)];
         const int nv = k < N ? NZ : 5;
 #pragma unroll
         for (int i = 0; i < NZ; ++i)
             if (i < nv) H[hx(i, i)] += X.delta;
-        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         const unsigned act = mode == 0 ? 0u : (unsigned)L[Y.oTACT + k];
         for_rows(k, N, X.fin, [&](int kind, int j) {
             const double w = mode == 0 ? L[Y.oLAM + NR * k + j] / L[Y.oS + NR * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
@@ -858,10 +863,10 @@ __device__ inline void load_bwd(const Ctx& X, int ogl, int k, int me, BwdRec& R)
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        R.gw[i] = L[ogl + NZ * k + 5 + i];
+        R.gw[i] = L[ogl + ZS * k + 5 + i];
         R.Kcol[i] = L[Y.oK + 15 * k + 5 * i + me];
     }
-    R.gx = L[ogl + NZ * k + me];
+    R.gx = L[ogl + ZS * k + me];
 }
 __device__ inline void load_fwd(const Ctx& X, int k, int me, FwdRec& R) {
     ldsd* L = X.L;
@@ -885,7 +890,7 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     const int me = X.ln < 5 ? X.ln : 0;
     double p[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) p[i] = L[ogl + NZ * N + i];
+    for (int i = 0; i < 5; ++i) p[i] = L[ogl + ZS * N + i];
     BwdRec cur, nxt;
     load_bwd(X, ogl, N - 1, me, cur);
     for (int k = N - 1; k >= 0; --k) {
@@ -907,7 +912,7 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         chol3_solve(cur.Lc, t);
         if (X.ln == 0)
 #pragma unroll
-            for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = t[i];
+            for (int i = 0; i < 3; ++i) L[odz + ZS * k + 5 + i] = t[i];
         if (k > 0) {
             double v = cur.gx;
 #pragma unroll
@@ -930,7 +935,7 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         double w[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            double v = L[odz + NZ * k + 5 + i];
+            double v = L[odz + ZS * k + 5 + i];
 #pragma unroll
             for (int l = 0; l < 5; ++l) v += fc.K[5 * i + l] * x[l];
             w[i] = v;
@@ -946,9 +951,9 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         for (int i = 0; i < 5; ++i) xn[i] = bcast(v, i);
         if (X.ln == 0) {
 #pragma unroll
-            for (int i = 0; i < 5; ++i) L[odz + NZ * k + i] = x[i];
+            for (int i = 0; i < 5; ++i) L[odz + ZS * k + i] = x[i];
 #pragma unroll
-            for (int i = 0; i < 3; ++i) L[odz + NZ * k + 5 + i] = w[i];
+            for (int i = 0; i < 3; ++i) L[odz + ZS * k + 5 + i] = w[i];
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) x[i] = xn[i];
@@ -956,9 +961,9 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     }
     if (X.ln == 0) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) L[odz + NZ * N + i] = x[i];
+        for (int i = 0; i < 5; ++i) L[odz + ZS * N + i] = x[i];
 #pragma unroll
-        for (int i = 5; i < NZ; ++i) L[odz + NZ * N + i] = 0.0;
+        for (int i = 5; i < NZ; ++i) L[odz + ZS * N + i] = 0.0;
     }
 }
 
@@ -972,7 +977,7 @@ __device__ inline double ab_at(const Ctx& X, int k, int l, int j) {
 __device__ inline double ht_at(const Ctx& X, int k, int u, int w) {
     const int sl = hs_slot(u, w);
     if (sl >= 0) return X.L[X.Y.oHS + 8 * k + sl];
-    const double h = X.L[X.Y.oH + NH * k + hidx(u, w)];
+    const double h = X.L[X.Y.oH + HSTR * k + hidx(u, w)];
     return (u == w && u < (k < X.N ? NZ : 5)) ? h + X.delta : h;
 }
 
@@ -1055,17 +1060,17 @@ __device__ bool factor_par(const Ctx& X) {
         for (int c = 0; c < 2; ++c) {
             for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) L[Y.oGL + NZ * k + i] = (k == N && i == (c == 0 ? 0 : 4)) ? 1.0 : 0.0;
+                for (int i = 0; i < NZ; ++i) L[Y.oGL + ZS * k + i] = (k == N && i == (c == 0 ? 0 : 4)) ? 1.0 : 0.0;
             sync();
             solve_core(X, Y.oGL, Y.oDZ);
             sync();
             for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) L[Y.oEZ + 2 * NZ * k + NZ * c + i] = L[Y.oDZ + NZ * k + i];
+                for (int i = 0; i < NZ; ++i) L[Y.oEZ + 2 * ZS * k + ZS * c + i] = L[Y.oDZ + ZS * k + i];
             sync();
         }
-        const double e0 = L[Y.oEZ + 2 * NZ * N + 0], e1 = L[Y.oEZ + 2 * NZ * N + NZ + 0];
-        const double e2 = L[Y.oEZ + 2 * NZ * N + 4], e3 = L[Y.oEZ + 2 * NZ * N + NZ + 4];
+        const double e0 = L[Y.oEZ + 2 * ZS * N + 0], e1 = L[Y.oEZ + 2 * ZS * N + ZS + 0];
+        const double e2 = L[Y.oEZ + 2 * ZS * N + 4], e3 = L[Y.oEZ + 2 * ZS * N + ZS + 4];
         if (ln == 0) {
             L[Y.oSC + SC_EM0] = e0;
             L[Y.oSC + SC_EM1] = e1;
@@ -1105,7 +1110,7 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     sync();
     double n0 = 0.0, n1 = 0.0;
     if (X.fin) {
-        const double b0 = rE[0] - L[Y.oDZ + NZ * N + 0], b1 = rE[1] - L[Y.oDZ + NZ * N + 4];
+        const double b0 = rE[0] - L[Y.oDZ + ZS * N + 0], b1 = rE[1] - L[Y.oDZ + ZS * N + 4];
         const double e0 = L[Y.oSC + SC_EM0], e1 = L[Y.oSC + SC_EM1], e2 = L[Y.oSC + SC_EM2], e3 = L[Y.oSC + SC_EM3];
         const double det = e0 * e3 - e1 * e2;
         n0 = (b0 * e3 - e1 * b1) / det;
@@ -1118,7 +1123,7 @@ __device__ void solve(Ctx& X, const double rE[2]) {
         for (int k = X.ln; k <= N; k += WAVE)
 #pragma unroll
             for (int i = 0; i < NZ; ++i)
-                L[Y.oDZ + NZ * k + i] += X.nu[0] * L[Y.oEZ + 2 * NZ * k + i] + X.nu[1] * L[Y.oEZ + 2 * NZ * k + NZ + i];
+                L[Y.oDZ + ZS * k + i] += X.nu[0] * L[Y.oEZ + 2 * ZS * k + i] + X.nu[1] * L[Y.oEZ + 2 * ZS * k + ZS + i];
     sync();
 }
 
@@ -1136,9 +1141,9 @@ __device__ void rollout(const Ctx& X, int oz) {
     for (int k = 0; k <= N; ++k) {
         if (X.ln == 0) {
 #pragma unroll
-            for (int i = 0; i < 5; ++i) L[oz + NZ * k + i] = x[i];
+            for (int i = 0; i < 5; ++i) L[oz + ZS * k + i] = x[i];
 #pragma unroll
-            for (int i = 5; i < NZ; ++i) L[oz + NZ * k + i] = 0.0;
+            for (int i = 5; i < NZ; ++i) L[oz + ZS * k + i] = 0.0;
         }
         if (k == N) break;
         double v = L[Y.oC + 5 * k + me];
@@ -1155,12 +1160,12 @@ __device__ void grad_f(const Ctx& X, int k, int oz, double g[NZ]) {
     const int nv = k < X.N ? NZ : 5;
     double z[NZ], H[NH];
 #pragma unroll
-    for (int i = 0; i < NZ; ++i) z[i] = X.L[oz + NZ * k + i];
+    for (int i = 0; i < NZ; ++i) z[i] = X.L[oz + ZS * k + i];
 #pragma unroll
-    for (int i = 0; i < NH; ++i) H[i] = X.L[X.Y.oH + NH * k + i];
+    for (int i = 0; i < NH; ++i) H[i] = X.L[X.Y.oH + HSTR * k + i];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
-        double v = X.L[X.Y.oGQ + NZ * k + i] + (i < nv ? X.delta * z[i] : 0.0);
+        double v = X.L[X.Y.oGQ + ZS * k + i] + (i < nv ? X.delta * z[i] : 0.0);
 #pragma unroll
         for (int j = 0; j < NZ; ++j) v += H[hidx(i, j)] * z[j];
         g[i] = i < nv ? v : 0.0;
@@ -1185,8 +1190,8 @@ __device__ int eqp(Ctx& X, double scale) {
             double g[NZ], z[NZ];
             grad_f(X, k, Y.oTZ, g);
 #pragma unroll
-            for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + NZ * k + u];
-            const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+            for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
+            const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
             const unsigned act = (unsigned)L[Y.oTACT + k];
             for_rows(k, N, X.fin, [&](int kind, int j) {
                 if (!((act >> j) & 1u)) return;
@@ -1196,19 +1201,19 @@ __device__ int eqp(Ctx& X, double scale) {
                 if (r.two) g[r.i1] += f * r.c1;
             });
 #pragma unroll
-            for (int u = 0; u < NZ; ++u) L[Y.oGL + NZ * k + u] = g[u];
+            for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
         }
         sync();
-        const double rE[2] = {X.e[0] - L[Y.oTZ + NZ * N + 0], X.e[1] - L[Y.oTZ + NZ * N + 4]};
+        const double rE[2] = {X.e[0] - L[Y.oTZ + ZS * N + 0], X.e[1] - L[Y.oTZ + ZS * N + 4]};
         solve(X, rE);
         double upd = 0.0, ym = 0.0;
         for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
-            for (int u = 0; u < NZ; ++u) L[Y.oTZ + NZ * k + u] += L[Y.oDZ + NZ * k + u];
+            for (int u = 0; u < NZ; ++u) L[Y.oTZ + ZS * k + u] += L[Y.oDZ + ZS * k + u];
             double z[NZ];
 #pragma unroll
-            for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + NZ * k + u];
-            const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+            for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
+            const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
             const unsigned act = (unsigned)L[Y.oTACT + k];
             for_rows(k, N, X.fin, [&](int kind, int j) {
                 if ((act >> j) & 1u) {
@@ -1231,12 +1236,12 @@ __device__ int eqp(Ctx& X, double scale) {
     const double tr = 1e-9 * scale, tl = 1e-9 * scale;
     for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
-        for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oTZ + NZ * k + u]) ? fin : 0.0;
+        for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oTZ + ZS * k + u]) ? fin : 0.0;
         unsigned mask = (unsigned)L[Y.oTACT + k];
         double z[NZ];
 #pragma unroll
-        for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + NZ * k + u];
-        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
+        const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         for_rows(k, N, X.fin, [&](int kind, int j) {
             const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
             if ((mask >> j) & 1u) {
@@ -1268,8 +1273,8 @@ __device__ int ipm(Ctx& X, int* iters) {
     for (int k = X.ln; k <= N; k += WAVE) {
         double z[NZ];
 #pragma unroll
-        for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + NZ * k + u];
-        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
+        const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         for_rows(k, N, X.fin, [&](int kind, int j) {
             const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
             L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
@@ -1292,7 +1297,7 @@ __device__ int ipm(Ctx& X, int* iters) {
         if (mu <= X.P.tol && phi <= 1e-12) { rc = 0; break; }
         if (X.dbg & 1) (void)factor_reg(X, 0);
         if (!factor_reg(X, 0)) { rc = -1; break; }
-        const double rE[2] = {X.e[0] - L[Y.oZ + NZ * N + 0], X.e[1] - L[Y.oZ + NZ * N + 4]};
+        const double rE[2] = {X.e[0] - L[Y.oZ + ZS * N + 0], X.e[1] - L[Y.oZ + ZS * N + 4]};
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
             if (pass == 1) {
@@ -1322,8 +1327,8 @@ __device__ int ipm(Ctx& X, int* iters) {
                 double g[NZ], z[NZ];
                 grad_f(X, k, Y.oZ, g);
 #pragma unroll
-                for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + NZ * k + u];
-                const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+                for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
+                const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
                 for_rows(k, N, X.fin, [&](int kind, int j) {
                     const RowSp r = row_sp(kind, k < N, kb, vb);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
@@ -1335,7 +1340,7 @@ __device__ int ipm(Ctx& X, int* iters) {
                     if (r.two) g[r.i1] -= f * r.c1;
                 });
 #pragma unroll
-                for (int u = 0; u < NZ; ++u) L[Y.oGL + NZ * k + u] = g[u];
+                for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
             }
             sync();
             if (X.dbg & 2) solve(X, rE);
@@ -1346,10 +1351,10 @@ __device__ int ipm(Ctx& X, int* iters) {
                 double z[NZ], dz[NZ];
 #pragma unroll
                 for (int u = 0; u < NZ; ++u) {
-                    z[u] = L[Y.oZ + NZ * k + u];
-                    dz[u] = L[Y.oDZ + NZ * k + u];
+                    z[u] = L[Y.oZ + ZS * k + u];
+                    dz[u] = L[Y.oDZ + ZS * k + u];
                 }
-                const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+                const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
                 for_rows(k, N, X.fin, [&](int kind, int j) {
                     const RowSp r = row_sp(kind, k < N, kb, vb);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
@@ -1373,7 +1378,7 @@ __device__ int ipm(Ctx& X, int* iters) {
                 if (dl < 0.0) amax = fmin(amax, -L[Y.oLAM + NR * k + j] / dl);
             }
 #pragma unroll
-            for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oDZ + NZ * k + u]) ? fin : 0.0;
+            for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oDZ + ZS * k + u]) ? fin : 0.0;
         }
         amax = wmin(amax);
         fin = wmin(fin);
@@ -1381,7 +1386,7 @@ __device__ int ipm(Ctx& X, int* iters) {
         if (!isfinite(alpha) || fin == 0.0) { rc = -1; break; }
         for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
-            for (int u = 0; u < NZ; ++u) L[Y.oZ + NZ * k + u] += alpha * L[Y.oDZ + NZ * k + u];
+            for (int u = 0; u < NZ; ++u) L[Y.oZ + ZS * k + u] += alpha * L[Y.oDZ + ZS * k + u];
             const int nr = stage_nrows(k, N, X.fin);
             for (int j = 0; j < nr; ++j) {
                 L[Y.oS + NR * k + j] += alpha * L[Y.oDS + NR * k + j];
@@ -1402,7 +1407,7 @@ __device__ void accept_polish(const Ctx& X, bool with_act) {
     const Layout& Y = X.Y;
     for (int k = X.ln; k <= X.N; k += WAVE) {
 #pragma unroll
-        for (int u = 0; u < NZ; ++u) L[Y.oZ + NZ * k + u] = L[Y.oTZ + NZ * k + u];
+        for (int u = 0; u < NZ; ++u) L[Y.oZ + ZS * k + u] = L[Y.oTZ + ZS * k + u];
 #pragma unroll
         for (int j = 0; j < NR; ++j) L[Y.oLAM + NR * k + j] = L[Y.oTLAM + NR * k + j];
         if (with_act) L[Y.oACT + k] = L[Y.oTACT + k];
@@ -1479,7 +1484,7 @@ __device__ void multipliers(Ctx& X) {
         grad_f(X, k, Y.oZ, g);
         L[Y.oMLAT + 2 * k] = 0.0;
         L[Y.oMLAT + 2 * k + 1] = 0.0;
-        const double kb = L[Y.oZB + NZ * k + 3], vb = L[Y.oZB + NZ * k + 4];
+        const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         for_rows(k, N, X.fin, [&](int kind, int j) {
             const RowSp r = row_sp(kind, k < N, kb, vb);
             const double l = L[Y.oLAM + NR * k + j];
@@ -1489,7 +1494,7 @@ __device__ void multipliers(Ctx& X) {
             if (kind == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
         });
 #pragma unroll
-        for (int u = 0; u < 5; ++u) L[Y.oGL + NZ * k + u] = g[u];
+        for (int u = 0; u < 5; ++u) L[Y.oGL + ZS * k + u] = g[u];
     }
     sync();
     // co-states: PI[k] = pi_{k+1} (one entry per lane on lanes 0..4, broadcast by readlane; lane 0 stores)
@@ -1497,7 +1502,7 @@ __device__ void multipliers(Ctx& X) {
         const int me = X.ln < 5 ? X.ln : 0;
         double pi[5];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) pi[i] = L[Y.oGL + NZ * N + i];
+        for (int i = 0; i < 5; ++i) pi[i] = L[Y.oGL + ZS * N + i];
         if (X.fin) {
             pi[0] += X.nu[0];
             pi[4] += X.nu[1];
@@ -1507,7 +1512,7 @@ __device__ void multipliers(Ctx& X) {
 #pragma unroll
                 for (int i = 0; i < 5; ++i) L[Y.oPI + 5 * k + i] = pi[i];
             if (k > 0) {
-                double v = L[Y.oGL + NZ * k + me];
+                double v = L[Y.oGL + ZS * k + me];
 #pragma unroll
                 for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + me] * pi[l];
 #pragma unroll
@@ -1521,10 +1526,10 @@ __device__ void multipliers(Ctx& X) {
         double xa[5], xb[5], D1[25], D1t[25], y[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-            xa[i] = L[Y.oZB + NZ * k + i];
-            xb[i] = L[Y.oZB + NZ * (k + 1) + i];
+            xa[i] = L[Y.oZB + ZS * k + i];
+            xb[i] = L[Y.oZB + ZS * (k + 1) + i];
         }
-        interval_jac(X, xa, xb, L[Y.oZB + NZ * k + 5], L[Y.oZB + NZ * k + 6], D1, nullptr);
+        interval_jac(X, xa, xb, L[Y.oZB + ZS * k + 5], L[Y.oZB + ZS * k + 6], D1, nullptr);
 #pragma unroll
         for (int i = 0; i < 5; ++i)
 #pragma unroll
@@ -1545,7 +1550,7 @@ __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const plan_params& P = X.P;
-    auto zv = [&](int k, int i) { return L[Y.oZB + NZ * k + i] + (alpha != 0.0 ? alpha * L[Y.oDZV + NZ * k + i] : 0.0); };
+    auto zv = [&](int k, int i) { return L[Y.oZB + ZS * k + i] + (alpha != 0.0 ? alpha * L[Y.oDZV + ZS * k + i] : 0.0); };
     double c = 0.0, v = 0.0;
     if (X.ln == 0)
         for (int i = 0; i < 5; ++i) v += fabs(zv(0, i) - X.x0[i]);
@@ -1602,10 +1607,10 @@ __device__ double cost_dir(const Ctx& X) {
     const plan_params& P = X.P;
     double v = 0.0;
     for (int k = X.ln; k < N; k += WAVE) {
-        v += 2.0 * P.w_y * (L[Y.oZB + NZ * k + 1] * L[Y.oDZV + NZ * k + 1] + L[Y.oZB + NZ * k + 2] * L[Y.oDZV + NZ * k + 2]);
-        v += -2.0 * P.w_s * (X.R.s_total - L[Y.oZB + NZ * k]) / (X.den * X.den) * L[Y.oDZV + NZ * k];
-        v += 2.0 * P.w_u * (L[Y.oZB + NZ * k + 5] * L[Y.oDZV + NZ * k + 5] + L[Y.oZB + NZ * k + 6] * L[Y.oDZV + NZ * k + 6]);
-        v += 2.0 * P.w_slack * L[Y.oZB + NZ * k + 7] * L[Y.oDZV + NZ * k + 7];
+        v += 2.0 * P.w_y * (L[Y.oZB + ZS * k + 1] * L[Y.oDZV + ZS * k + 1] + L[Y.oZB + ZS * k + 2] * L[Y.oDZV + ZS * k + 2]);
+        v += -2.0 * P.w_s * (X.R.s_total - L[Y.oZB + ZS * k]) / (X.den * X.den) * L[Y.oDZV + ZS * k];
+        v += 2.0 * P.w_u * (L[Y.oZB + ZS * k + 5] * L[Y.oDZV + ZS * k + 5] + L[Y.oZB + ZS * k + 6] * L[Y.oDZV + ZS * k + 6]);
+        v += 2.0 * P.w_slack * L[Y.oZB + ZS * k + 7] * L[Y.oDZV + ZS * k + 7];
     }
     return wsum(v);
 }
@@ -1672,11 +1677,11 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
     const double dss = (X.st - X.x0[0]) / N;
     for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) L[Y.oZB + NZ * k + i] = 0.0;
-        L[Y.oZB + NZ * k + 0] = k == N ? X.st : X.x0[0] + k * dss;
-        L[Y.oZB + NZ * k + 4] = X.fin ? (k == N ? 0.0 : X.x0[4] + k * ((0.0 - X.x0[4]) / N)) : X.x0[4];
+        for (int i = 0; i < NZ; ++i) L[Y.oZB + ZS * k + i] = 0.0;
+        L[Y.oZB + ZS * k + 0] = k == N ? X.st : X.x0[0] + k * dss;
+        L[Y.oZB + ZS * k + 4] = X.fin ? (k == N ? 0.0 : X.x0[4] + k * ((0.0 - X.x0[4]) / N)) : X.x0[4];
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) L[Y.oZ2 + NZ * k + i] = L[Y.oZB + NZ * k + i];
+        for (int i = 0; i < NZ; ++i) L[Y.oZ2 + ZS * k + i] = L[Y.oZB + ZS * k + i];
     }
     sync();
     int status = PLAN_NOT_CONVERGED, total = 0, nq = 0, since = 0;
@@ -1705,8 +1710,8 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         for (int k = X.ln; k <= N; k += WAVE) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i) {
-                const double d = (k < N || i < 5) ? L[Y.oZ + NZ * k + i] : 0.0;
-                L[Y.oDZV + NZ * k + i] = d;
+                const double d = (k < N || i < 5) ? L[Y.oZ + ZS * k + i] : 0.0;
+                L[Y.oDZV + ZS * k + i] = d;
                 full = fmax(full, fabs(d));
             }
             if (k < N)
@@ -1721,7 +1726,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         sync();
         double alpha = 1.0;
         if (full > LS_FULL) {
-            for (int k = X.ln; k <= N; k += WAVE) L[Y.oVL + k] = frozen ? L[Y.oVLIM + k] : route_vmax(X.R, L[Y.oZB + NZ * k]);
+            for (int k = X.ln; k <= N; k += WAVE) L[Y.oVL + k] = frozen ? L[Y.oVLIM + k] : route_vmax(X.R, L[Y.oZB + ZS * k]);
             sync();
             double f0, v0;
             cost_viol(X, 0.0, &f0, &v0);
@@ -1744,10 +1749,10 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 if (k == N && i >= 5) continue;
-                const double zo = L[Y.oZB + NZ * k + i];
-                const double zn = zo + alpha * L[Y.oDZV + NZ * k + i];
+                const double zo = L[Y.oZB + ZS * k + i];
+                const double zn = zo + alpha * L[Y.oDZV + ZS * k + i];
                 step = fmax(step, fabs(zn - zo));
-                back2 = fmax(back2, fabs(zn - L[Y.oZ2 + NZ * k + i]));
+                back2 = fmax(back2, fabs(zn - L[Y.oZ2 + ZS * k + i]));
                 fin = isfinite(zn) ? fin : 0.0;
             }
         step = wmax(step);
@@ -1758,9 +1763,9 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 if (k == N && i >= 5) continue;
-                const double zo = L[Y.oZB + NZ * k + i];
-                L[Y.oZ2 + NZ * k + i] = zo;
-                L[Y.oZB + NZ * k + i] = zo + alpha * L[Y.oDZV + NZ * k + i];
+                const double zo = L[Y.oZB + ZS * k + i];
+                L[Y.oZ2 + ZS * k + i] = zo;
+                L[Y.oZB + ZS * k + i] = zo + alpha * L[Y.oDZV + ZS * k + i];
             }
         sync();
         last = step;
@@ -1768,19 +1773,19 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         if (since >= 2 && back2 <= CYCLE_REL * step) {
             if (frozen) break;
             for (int k = X.ln; k <= N; k += WAVE)
-                L[Y.oVLIM + k] = fmin(route_vmax(X.R, L[Y.oZB + NZ * k]), route_vmax(X.R, L[Y.oZ2 + NZ * k]));
+                L[Y.oVLIM + k] = fmin(route_vmax(X.R, L[Y.oZB + ZS * k]), route_vmax(X.R, L[Y.oZ2 + ZS * k]));
             frozen = true;
             since = -1;
             for (int k = X.ln; k <= N; k += WAVE)
 #pragma unroll
-                for (int i = 0; i < NZ; ++i) L[Y.oZ2 + NZ * k + i] = L[Y.oZB + NZ * k + i];
+                for (int i = 0; i < NZ; ++i) L[Y.oZ2 + ZS * k + i] = L[Y.oZB + ZS * k + i];
             sync();
         }
     }
     if (status == PLAN_FROZEN_LIMITS) {
         double bad = 0.0;
         for (int k = X.ln; k <= N; k += WAVE)
-            if (L[Y.oZB + NZ * k + 4] + (k < N ? L[Y.oZB + NZ * k + 7] : 0.0) > route_vmax(X.R, L[Y.oZB + NZ * k]) + 1e-9)
+            if (L[Y.oZB + ZS * k + 4] + (k < N ? L[Y.oZB + ZS * k + 7] : 0.0) > route_vmax(X.R, L[Y.oZB + ZS * k]) + 1e-9)
                 bad = 1.0;
         if (wmax(bad) > 0.0) status = PLAN_NOT_CONVERGED;
     }
@@ -1789,13 +1794,13 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
     for (int k = X.ln; k <= Nm; k += WAVE) {
         if (a.X)
 #pragma unroll
-            for (int i = 0; i < 5; ++i) a.X[((size_t)b * (Nm + 1) + k) * 5 + i] = k <= N ? L[Y.oZB + NZ * k + i] : 0.0;
+            for (int i = 0; i < 5; ++i) a.X[((size_t)b * (Nm + 1) + k) * 5 + i] = k <= N ? L[Y.oZB + ZS * k + i] : 0.0;
         if (k < Nm) {
             if (a.U) {
-                a.U[((size_t)b * Nm + k) * 2 + 0] = k < N ? L[Y.oZB + NZ * k + 5] : 0.0;
-                a.U[((size_t)b * Nm + k) * 2 + 1] = k < N ? L[Y.oZB + NZ * k + 6] : 0.0;
+                a.U[((size_t)b * Nm + k) * 2 + 0] = k < N ? L[Y.oZB + ZS * k + 5] : 0.0;
+                a.U[((size_t)b * Nm + k) * 2 + 1] = k < N ? L[Y.oZB + ZS * k + 6] : 0.0;
             }
-            if (a.S) a.S[(size_t)b * Nm + k] = k < N ? L[Y.oZB + NZ * k + 7] : 0.0;
+            if (a.S) a.S[(size_t)b * Nm + k] = k < N ? L[Y.oZB + ZS * k + 7] : 0.0;
         }
     }
     if (X.ln == 0) {
