@@ -109,6 +109,43 @@ def from_waypoints(points, max_speed, name="route"):
     return Route(det, speed_limit_array(pts, det, max_speed), name)
 
 
+# WGS84 (pymap3d's default ellipsoid, which path_planning.global2local uses through geodetic2enu)
+_WGS84_A = 6378137.0
+_WGS84_F = 1.0 / 298.257223563
+
+
+def _geodetic2ecef(lat, lon, h):
+    e2 = _WGS84_F * (2.0 - _WGS84_F)
+    la, lo = np.radians(lat), np.radians(lon)
+    n = _WGS84_A / np.sqrt(1.0 - e2 * np.sin(la) ** 2)
+    return ((n + h) * np.cos(la) * np.cos(lo), (n + h) * np.cos(la) * np.sin(lo), (n * (1.0 - e2) + h) * np.sin(la))
+
+
+def global2local(points):
+    """path_planning.global2local (:91-108): (lon, lat) way-points to local east/north metres with the first
+    point as origin (geodetic -> ECEF -> ENU on WGS84, altitude 0; pymap3d is not installed here, so the
+    projection is restated)."""
+    lon0, lat0 = points[0]
+    x0, y0, z0 = _geodetic2ecef(lat0, lon0, 0.0)
+    la0, lo0 = np.radians(lat0), np.radians(lon0)
+    out = []
+    for lon, lat in points:
+        x, y, z = _geodetic2ecef(lat, lon, 0.0)
+        dx, dy, dz = x - x0, y - y0, z - z0
+        east = -np.sin(lo0) * dx + np.cos(lo0) * dy
+        north = -np.sin(la0) * np.cos(lo0) * dx - np.sin(la0) * np.sin(lo0) * dy + np.cos(la0) * dz
+        out.append((float(east), float(north)))
+    return out
+
+
+def from_graphhopper(route, name="route"):
+    """The route dict path_planning.get_route returns (:50-88: 'points' as (lon, lat), 'max_speed' details
+    [[start, end, km/h or None]] over them), projected and densified as get_path_and_speed_limits does
+    (:170-262).  Fetching it (GraphHopper over HTTP) stays out of scope."""
+    pts = global2local([(float(lon), float(lat)) for lon, lat in route["points"]])
+    return from_waypoints(pts, [tuple(iv) for iv in route.get("max_speed", [])], name)
+
+
 def global_line(X):
     """The global (x, y) line of a committed trajectory, integrated like trajectory_loader.py:32-62."""
     s = X[:, 0].copy()

@@ -106,11 +106,15 @@ class TrajectoryOptimizer:
 
 def optimize_full_trajectory(route, max_chunk_size=20, max_chunks=10000, device=0, verbose=False, check=True,
                              solve_chunk=None):
-    """The chunked receding-horizon planner of trajectory_planning.py:419-559 on a routes.Route: returns
+    """The chunked receding-horizon planner of trajectory_planning.py:419-559 on a routes.Route (or the
+    reference's GraphHopper route dict, converted by routes.from_graphhopper): returns
     (X, U, S) and runs the restated reference_trajectory_check on the result (:557).  max_chunks caps the
     loop (the reference has no cap); per-chunk statuses and horizons are left in
     `optimize_full_trajectory.statuses` / `.horizons`.  solve_chunk(x0, s_target, is_final, N) -> (X, U, S,
     status) replaces the GPU chunk solve (tests drive this loop with the CPU oracle)."""
+    if isinstance(route, dict):                               # the reference's GraphHopper route object
+        import routes
+        route = routes.from_graphhopper(route)
     v_min_fun = lambda s: 0                                   # :476-477
     X_full, U_full, S_full, statuses, horizons = [], [], [], [], []
     current_x0 = np.array([0.0, 0.0, 0.0, 0.0, 0.0])          # :486

@@ -34,3 +34,27 @@ def test_rank_shards_make_up_the_batch():
     key = lambda w: sorted(map(tuple, np.column_stack([w["x0"], w["s_target"], w["is_final"], w["N"]]).tolist()))
     merged = {k: np.concatenate([p[k] for p in parts]) for k in ("x0", "s_target", "is_final", "N")}
     assert key(merged) == key(full)
+
+
+def test_graphhopper_route_dict_is_accepted():
+    """optimize_full_trajectory takes the reference's own route object (path_planning.get_route's dict:
+    (lon, lat) points and max_speed details): routes.from_graphhopper projects it to local metres as
+    global2local does (WGS84 ENU, first point at the origin) and builds the same route as from_waypoints."""
+    import routes
+    pts = [(-73.5673, 45.5017), (-73.5660, 45.5025), (-73.5640, 45.5030), (-73.5631, 45.5049)]
+    loc = routes.global2local(pts)
+    assert loc[0] == (0.0, 0.0)
+    # local tangent plane vs the small-distance approximation (east = R_N cos(lat) dlon, north = R_M dlat)
+    a, f = 6378137.0, 1 / 298.257223563
+    e2 = f * (2 - f)
+    lat0 = np.radians(45.5017)
+    rn = a / np.sqrt(1 - e2 * np.sin(lat0) ** 2)
+    rm = a * (1 - e2) / (1 - e2 * np.sin(lat0) ** 2) ** 1.5
+    for (lon, lat), (e, n) in zip(pts, loc):
+        assert abs(e - rn * np.cos(lat0) * np.radians(lon + 73.5673)) < 0.05
+        assert abs(n - rm * np.radians(lat - 45.5017)) < 0.05
+    ms = [[0, 2, 50], [2, 3, None]]
+    r1 = routes.from_graphhopper({"points": pts, "max_speed": ms})
+    r2 = routes.from_waypoints(loc, [tuple(m) for m in ms])
+    assert np.array_equal(r1.s, r2.s) and np.array_equal(r1.vmax, r2.vmax)
+    assert np.isclose(r1.vmax[0], 50 / 3.6) and np.isclose(r1.vmax[-1], 30 / 3.6)
