@@ -172,3 +172,76 @@ def optimize_full_trajectory(route, max_chunk_size=20, max_chunks=10000, device=
     for pl in opt._planners.values():
         pl.close()
     return X_final, U_final, S_final
+
+
+def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=10000, device=0, solve_chunks=None):
+    """The chunk loop of optimize_full_trajectory (trajectory_planning.py:491-548) for B plans on one route at
+    once, from B start states (e.g. a fleet re-planning from where each vehicle is): every round solves the
+    current chunk of each unfinished plan in one batched call, each chunk with its own horizon (the
+    reference's N rule) and its own final-chunk flag.  Plan b follows exactly the chunk sequence
+    optimize_full_trajectory would run from starts[b] (start (0, 0, 0, 0, 0) = the reference's).
+
+    Returns (plans, summary): plans[b] = (X, U, S); summary[b] = sanity_checks.plan_check_summary of the plan
+    plus 'statuses' and 'horizons' of its chunks.  solve_chunks(x0 [n,5], s_target [n], is_final [n], N [n])
+    -> dict(X, U, S, status) replaces the GPU batch (tests drive this loop with the CPU oracle)."""
+    from sanity_checks import plan_check_summary
+    if isinstance(route, dict):
+        import routes
+        route = routes.from_graphhopper(route)
+    starts = np.atleast_2d(np.asarray(starts, np.float64))
+    B = starts.shape[0]
+    s_total = route.s_total
+    cur = starts.copy()
+    pieces = [[] for _ in range(B)]
+    statuses = [[] for _ in range(B)]
+    horizons = [[] for _ in range(B)]
+    done = np.zeros(B, bool)
+    opt = TrajectoryOptimizer(device=device)
+    pl = None
+    for _ in range(max_chunks):
+        act = np.flatnonzero(~done & (s_total - cur[:, 0] > 0.1))
+        done[~done & (s_total - cur[:, 0] <= 0.1)] = True
+        if act.size == 0:
+            break
+        rem = s_total - cur[act, 0]
+        fin = (rem < max_chunk_size * 2).astype(np.int32)
+        size = np.where(fin == 1, rem, max_chunk_size)
+        st = cur[act, 0] + size
+        N = np.array([int(np.ceil(size[i] / route.avg_speed_from(cur[b, 0]) * 2.0 / 0.3))
+                      for i, b in enumerate(act)], np.int32)
+        if N.max() > mpcplan.PLAN_MAX_N:
+            raise ValueError(f"chunk horizon N={N.max()} exceeds PLAN_MAX_N={mpcplan.PLAN_MAX_N}")
+        if solve_chunks is None:
+            if pl is None:
+                opt.N, opt.dt = int(N.max()), 0.3
+                pl = mpcplan.Planner(route, opt.params(0.0), device=device)
+            r = pl.solve_chunks(cur[act], st, fin, N)
+        else:
+            r = solve_chunks(cur[act], st, fin, N)
+        for i, b in enumerate(act):
+            n = int(N[i])
+            X, U, S = r["X"][i, :n + 1], r["U"][i, :n], r["S"][i, :n]
+            statuses[b].append(int(r["status"][i]))
+            horizons[b].append(n)
+            if not fin[i]:                                              # :523-541
+                c = int(n / 2)
+                pieces[b].append((X[:c + 1] if not pieces[b] else X[1:c + 1], U[:c], S[:c]))
+            else:
+                pieces[b].append((X[1:], U, S))
+            cur[b] = pieces[b][-1][0][-1]
+    if pl is not None:
+        pl.close()
+    plans, summary = [], []
+    for b in range(B):
+        if not pieces[b]:
+            plans.append((starts[b][None], np.zeros((0, 2)), np.zeros(0)))
+            summary.append({"passed": False, "statuses": [], "horizons": []})
+            continue
+        X = np.concatenate([p[0] for p in pieces[b]])
+        U = np.concatenate([p[1] for p in pieces[b]])
+        S = np.concatenate([p[2] for p in pieces[b]])
+        plans.append((X, U, S))
+        q = plan_check_summary(opt.u_min, opt.u_max, X, U, S, s_total)
+        q["statuses"], q["horizons"] = statuses[b], horizons[b]
+        summary.append(q)
+    return plans, summary

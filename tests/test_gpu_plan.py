@@ -174,3 +174,25 @@ def test_device_horizon_out_of_range_is_flagged(env):
     for b in (0, 2, 4):
         assert sth[b] == h["status"][b] and np.array_equal(Xh[b], h["X"][b])
     pl.close()
+
+
+def test_batched_receding_loop_on_gpu(env, capsys):
+    """optimize_full_trajectory_batch on the GPU: 48 plans on trajectory1's route from starts spread along it
+    (the first at the reference's start) advance together, one launch per round; the first plan equals the
+    single-route loop's, and the plans reach the destination and pass the restated checks."""
+    mpcplan, PO, W = env
+    import trajectory_planning as TP
+    r = W.plan_route("traj1")
+    X1, U1, S1 = TP.optimize_full_trajectory(r, check=False)
+    rng = np.random.default_rng(4)
+    starts = np.zeros((48, 5))
+    for b in range(1, 48):
+        s0 = rng.uniform(1.0, r.s_total - 30.0)
+        starts[b] = (s0, rng.normal(0, 0.05), rng.normal(0, 0.01), r.k_ref_fun(s0), rng.uniform(0.2, 0.9) * r.v_max_fun(s0))
+    plans, summary = TP.optimize_full_trajectory_batch(r, starts)
+    assert np.array_equal(plans[0][0], X1) and np.array_equal(plans[0][1], U1)
+    passed = np.array([q["passed"] for q in summary])
+    print(f"batched GPU plans: {passed.sum()}/48 pass the checks, chunks per plan "
+          f"{min(len(q['statuses']) for q in summary)}-{max(len(q['statuses']) for q in summary)}")
+    assert passed.mean() >= 0.9
+    assert all(abs(p[0][-1, 0] - r.s_total) < 1e-3 for p in plans)

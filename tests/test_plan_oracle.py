@@ -122,3 +122,34 @@ def test_receding_horizon_loop_with_oracle_passes_check(env, capsys):
     assert "===> Checks passed : True" in out, out
     assert q["passed"] and abs(X[-1, 0] - r.s_total) < 1e-6 and abs(X[-1, 4]) < 1e-9
     assert np.isin(st, (0, 4)).mean() >= 0.9
+
+
+def test_batched_receding_loop_equals_the_single_loop(env, capsys):
+    """optimize_full_trajectory_batch: B plans on one route advance together, one batched chunk solve per
+    round with per-chunk horizons.  With the oracle as the batch solver, a plan from the reference's start
+    equals optimize_full_trajectory's plan exactly, and plans from other starts on the route reach the
+    destination and pass the restated checks."""
+    PO, PR, W = env
+    import trajectory_planning as TP
+    r = W.plan_route("synth1")
+    orc = PO.PlanOracle(r)
+
+    def solve_chunk(x0, st, fin, N):
+        o = orc.solve_batch(PO.default_params(N=N), np.asarray(x0)[None], st, int(fin))
+        return o["X"][0], o["U"][0], o["S"][0], o["status"][0]
+
+    def solve_chunks(x0, st, fin, N):
+        return orc.solve_batch(PO.default_params(N=int(N.max())), x0, st, fin, N=N, num_threads=8)
+
+    X1, U1, S1 = TP.optimize_full_trajectory(r, solve_chunk=solve_chunk, check=False)
+    starts = np.zeros((3, 5))
+    for b, s0 in ((1, 400.0), (2, 1100.0)):
+        starts[b] = (s0, 0.02, 0.0, r.k_ref_fun(s0), 0.6 * r.v_max_fun(s0))
+    plans, summary = TP.optimize_full_trajectory_batch(r, starts, solve_chunks=solve_chunks)
+    X, U, S = plans[0]
+    assert np.array_equal(X, X1) and np.array_equal(U, U1) and np.array_equal(S, S1)
+    assert summary[0]["statuses"] == TP.optimize_full_trajectory.statuses
+    for b in range(3):
+        assert summary[b]["passed"], (b, summary[b])
+        assert abs(plans[b][0][-1, 0] - r.s_total) < 1e-6
+    print("batched plans: chunks", [len(q["statuses"]) for q in summary])
