@@ -64,6 +64,9 @@ def main():
                          "optimize_full_trajectory poses them (20 m chunks, per-chunk horizon) on --plan-route; "
                          "reported as 'plan' in chunks/s, never as 'value' (0: skip)")
     ap.add_argument("--plan-steps", type=int, default=3, metavar="K")
+    ap.add_argument("--plan-fleet", type=int, default=1024, metavar="B",
+                    help="planner leg, secondary: B full plans on trajectory1's route from random starts, all "
+                         "advancing together (trajectory_planning.optimize_full_trajectory_batch), rank 0 only")
     ap.add_argument("--plan-route", default="traj3")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: a stand-in that runs the same sharded path on libmpcqp's host backend (device = -1) "
@@ -202,6 +205,8 @@ def main():
     # offline-planner leg on every rank (its own chunk shard)
     plan = plan_leg(args.plan_chunks, args.plan_steps, args.plan_route, world, rank, dev, args.cpu_seconds,
                     not args.no_cpu) if (args.plan_chunks and gpu) else None
+    if plan is not None and args.plan_fleet > 0:
+        plan["fleet"] = plan_fleet(args.plan_fleet, dev_index)
 
     if rank == 0:
         out = {
@@ -604,6 +609,32 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
             out["cpu_reference"] = plan_cpu_reference(r, wb)
     pl.close()
     return out
+
+
+def plan_fleet(B, device):
+    """B complete plans of trajectory1's route (the reference's chunk loop, :491-548) from random starts along
+    it, advancing together: one batched launch per round (trajectory_planning.optimize_full_trajectory_batch),
+    wall time including the host loop; the restated checks on every plan."""
+    import numpy as np
+    import trajectory_planning as TP
+    import workloads as W
+    r = W.plan_route("traj1")
+    rng = np.random.default_rng(11)
+    starts = np.zeros((B, 5))
+    for b in range(1, B):
+        s0 = rng.uniform(1.0, r.s_total - 30.0)
+        starts[b] = (s0, rng.normal(0, 0.05), rng.normal(0, 0.01), r.k_ref_fun(s0),
+                     rng.uniform(0.2, 0.9) * r.v_max_fun(s0))
+    t0 = time.perf_counter()
+    plans, summary = TP.optimize_full_trajectory_batch(r, starts, device=device)
+    dt = time.perf_counter() - t0
+    chunks = sum(len(q["statuses"]) for q in summary)
+    return {"plans": B, "seconds": dt, "plans_per_s": B / dt, "chunks": chunks, "chunks_per_s": chunks / dt,
+            "rounds": max(len(q["statuses"]) for q in summary),
+            "checks_passed": int(sum(bool(q["passed"]) for q in summary)),
+            "route": f"traj1 ({r.s_total:.0f} m), starts uniform along it (the first the reference's)",
+            "note": "wall time of the whole batched receding-horizon loop (host bookkeeping included); one "
+                    "launch per round over the unfinished plans"}
 
 
 def plan_cpu_baseline(route, wb, budget_s, status, groups):
