@@ -206,7 +206,10 @@ def main():
     plan = plan_leg(args.plan_chunks, args.plan_steps, args.plan_route, world, rank, dev, args.cpu_seconds,
                     not args.no_cpu) if (args.plan_chunks and gpu) else None
     if plan is not None and args.plan_fleet > 0:
-        plan["fleet"] = plan_fleet(args.plan_fleet, dev_index)
+        try:
+            plan["fleet"] = plan_fleet(args.plan_fleet, dev_index)
+        except Exception as e:      # a secondary leg never takes the headline line down with it
+            plan["fleet"] = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         out = {
