@@ -64,7 +64,7 @@ def main():
                          "optimize_full_trajectory poses them (20 m chunks, per-chunk horizon) on --plan-route; "
                          "reported as 'plan' in chunks/s, never as 'value' (0: skip)")
     ap.add_argument("--plan-steps", type=int, default=3, metavar="K")
-    ap.add_argument("--plan-fleet", type=int, default=1024, metavar="B",
+    ap.add_argument("--plan-fleet", type=int, default=0, metavar="B",
                     help="planner leg, secondary: B full plans on trajectory1's route from random starts, all "
                          "advancing together (trajectory_planning.optimize_full_trajectory_batch), rank 0 only")
     ap.add_argument("--plan-route", default="traj3")
