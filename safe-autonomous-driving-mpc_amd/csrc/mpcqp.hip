@@ -2225,6 +2225,9 @@ struct mpc_ctx {
     double* stc;
     size_t cap_stc;     // doubles
     bool use_stc;
+    // MPC_IPM_GL64=1: the N = 20 interior-point launch of the split path with one deferred instance per
+    // wavefront (GL = 64) instead of two (A/B switch)
+    bool ipm_gl64;
 };
 
 extern "C" void mpc_default_params(mpc_params* p) {
@@ -2351,6 +2354,8 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         c->use_stc = e2 && e2[0] == '1';
         const char* e3 = std::getenv("MPC_WL_MEMSET");
         c->wl_memset = e3 && e3[0] == '1';
+        const char* e4 = std::getenv("MPC_IPM_GL64");
+        c->ipm_gl64 = e4 && e4[0] == '1';
     }
     if (hipMalloc(&c->table_buf, h.size() * sizeof(double)) != hipSuccess) {
         std::free(c);
@@ -2526,7 +2531,20 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
         // the launched MODE_XO zeroed wl[epoch ^ 1] and uses wl[epoch]: the next eager call takes the other
         if (wnext) c->wl_epoch ^= 1;
-        MPC_LAUNCH_GL(MODE_IPM);
+        if (nt20 && c->ipm_gl64) {
+            // one deferred instance per wavefront: B waves at most, the wave's LDS for one group
+            const size_t lds_one = sizeof(double) * (size_t)lds_doubles(kp.N, true);
+            if (with_obs)
+                hipLaunchKernelGGL((mpc_solve_kernel<64, true, MODE_IPM, 20>), dim3(B), dim3(WAVE), lds_one, st,
+                                   c->tab, kp, B, x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt, stc,
+                                   nullptr);
+            else
+                hipLaunchKernelGGL((mpc_solve_kernel<64, false, MODE_IPM, 20>), dim3(B), dim3(WAVE), lds_one, st,
+                                   c->tab, kp, B, x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt, stc,
+                                   nullptr);
+        } else {
+            MPC_LAUNCH_GL(MODE_IPM);
+        }
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
         if (!capturing) {
             HIPCHK(hipEventRecord(c->wl_done, st), MPC_E_DEVICE);
