@@ -669,24 +669,24 @@ static int factor(const qp_t* Q, const double W[][NR], fac_t* F) {
         for (int i = 0; i < 5; ++i) {
             for (int j = 0; j < 5; ++j) {
                 double v = 0.0;
-                for (int l = 0; l < 5; ++l) v += P[5 * i + l] * A[5 * l + j];
+                for (int l = 0; l < 5; ++l) v = fma(P[5 * i + l], A[5 * l + j], v);
                 PA[5 * i + j] = v;
             }
             for (int j = 0; j < 3; ++j) {
                 double v = 0.0;
-                for (int l = 0; l < 5; ++l) v += P[5 * i + l] * B[3 * l + j];
+                for (int l = 0; l < 5; ++l) v = fma(P[5 * i + l], B[3 * l + j], v);
                 PB[3 * i + j] = v;
             }
         }
         for (int i = 0; i < 3; ++i) {
             for (int j = 0; j < 3; ++j) {
                 double v = H[5 + i][5 + j];
-                for (int l = 0; l < 5; ++l) v += B[3 * l + i] * PB[3 * l + j];
+                for (int l = 0; l < 5; ++l) v = fma(B[3 * l + i], PB[3 * l + j], v);
                 Hww[i][j] = v;
             }
             for (int j = 0; j < 5; ++j) {
                 double v = H[5 + i][j];
-                for (int l = 0; l < 5; ++l) v += B[3 * l + i] * PA[5 * l + j];
+                for (int l = 0; l < 5; ++l) v = fma(B[3 * l + i], PA[5 * l + j], v);
                 Hwx[5 * i + j] = v;
             }
         }
@@ -703,8 +703,8 @@ static int factor(const qp_t* Q, const double W[][NR], fac_t* F) {
             for (int i = 0; i < 5; ++i)
                 for (int j = 0; j < 5; ++j) {
                     double v = H[i][j];
-                    for (int l = 0; l < 5; ++l) v += A[5 * l + i] * PA[5 * l + j];
-                    for (int l = 0; l < 3; ++l) v += Hwx[5 * l + i] * F->K[k][5 * l + j];
+                    for (int l = 0; l < 5; ++l) v = fma(A[5 * l + i], PA[5 * l + j], v);
+                    for (int l = 0; l < 3; ++l) v = fma(Hwx[5 * l + i], F->K[k][5 * l + j], v);
                     Pn[5 * i + j] = v;
                 }
             for (int i = 0; i < 5; ++i)
@@ -748,7 +748,7 @@ static void solve_core(const qp_t* Q, const fac_t* F, const double gl[][NZ], dou
         double h[3];
         for (int i = 0; i < 3; ++i) {
             double v = gl[k][5 + i];
-            for (int l = 0; l < 5; ++l) v += B[3 * l + i] * p[l];
+            for (int l = 0; l < 5; ++l) v = fma(B[3 * l + i], p[l], v);
             h[i] = v;
         }
         double t[3] = {-h[0], -h[1], -h[2]};
@@ -758,8 +758,8 @@ static void solve_core(const qp_t* Q, const fac_t* F, const double gl[][NZ], dou
             double pn[5];
             for (int i = 0; i < 5; ++i) {
                 double v = gl[k][i];
-                for (int l = 0; l < 5; ++l) v += A[5 * l + i] * p[l];
-                for (int l = 0; l < 3; ++l) v += F->K[k][5 * l + i] * h[l];
+                for (int l = 0; l < 5; ++l) v = fma(A[5 * l + i], p[l], v);
+                for (int l = 0; l < 3; ++l) v = fma(F->K[k][5 * l + i], h[l], v);
                 pn[i] = v;
             }
             memcpy(p, pn, sizeof(p));
@@ -770,7 +770,7 @@ static void solve_core(const qp_t* Q, const fac_t* F, const double gl[][NZ], dou
         double w[3];
         for (int i = 0; i < 3; ++i) {
             double v = kk[k][i];
-            for (int l = 0; l < 5; ++l) v += F->K[k][5 * i + l] * x[l];
+            for (int l = 0; l < 5; ++l) v = fma(F->K[k][5 * i + l], x[l], v);
             w[i] = v;
         }
         for (int i = 0; i < 5; ++i) dz[k][i] = x[i];
@@ -778,8 +778,8 @@ static void solve_core(const qp_t* Q, const fac_t* F, const double gl[][NZ], dou
         double xn[5];
         for (int i = 0; i < 5; ++i) {
             double v = 0.0;
-            for (int l = 0; l < 5; ++l) v += Q->A[k][5 * i + l] * x[l];
-            for (int l = 0; l < 3; ++l) v += Q->B[k][3 * i + l] * w[l];
+            for (int l = 0; l < 5; ++l) v = fma(Q->A[k][5 * i + l], x[l], v);
+            for (int l = 0; l < 3; ++l) v = fma(Q->B[k][3 * i + l], w[l], v);
             xn[i] = v;
         }
         memcpy(x, xn, sizeof(x));

@@ -900,11 +900,11 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         {
             double v = cur.gw[0];
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v += cur.B0[l] * p[l];
+            for (int l = 0; l < 5; ++l) v = fma(cur.B0[l], p[l], v);
             h[0] = v;
             v = cur.gw[1];
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v += cur.B1[l] * p[l];
+            for (int l = 0; l < 5; ++l) v = fma(cur.B1[l], p[l], v);
             h[1] = v;
         }
         h[2] = cur.gw[2];
@@ -916,9 +916,9 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         if (k > 0) {
             double v = cur.gx;
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v += cur.Acol[l] * p[l];
+            for (int l = 0; l < 5; ++l) v = fma(cur.Acol[l], p[l], v);
 #pragma unroll
-            for (int l = 0; l < 3; ++l) v += cur.Kcol[l] * h[l];
+            for (int l = 0; l < 3; ++l) v = fma(cur.Kcol[l], h[l], v);
 #pragma unroll
             for (int i = 0; i < 5; ++i) p[i] = bcast(v, i);
         }
@@ -937,14 +937,14 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         for (int i = 0; i < 3; ++i) {
             double v = L[odz + ZS * k + 5 + i];
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v += fc.K[5 * i + l] * x[l];
+            for (int l = 0; l < 5; ++l) v = fma(fc.K[5 * i + l], x[l], v);
             w[i] = v;
         }
         double v = 0.0;
 #pragma unroll
-        for (int l = 0; l < 5; ++l) v += fc.Arow[l] * x[l];
+        for (int l = 0; l < 5; ++l) v = fma(fc.Arow[l], x[l], v);
 #pragma unroll
-        for (int l = 0; l < 2; ++l) v += fc.Brow[l] * w[l];
+        for (int l = 0; l < 2; ++l) v = fma(fc.Brow[l], w[l], v);
         // stage k overwritten after every lane has read its control part (the broadcast orders that)
         double xn[5];
 #pragma unroll
@@ -1011,11 +1011,11 @@ __device__ bool factor_par(const Ctx& X) {
                 for (int i = 0; i < 5; ++i) {
                     double v = 0.0;
 #pragma unroll
-                    for (int l = 0; l < 5; ++l) v += P[5 * i + l] * ab_at(X, k, l, w);
+                    for (int l = 0; l < 5; ++l) v = fma(P[5 * i + l], ab_at(X, k, l, w), v);
                     pab[i] = v;
                 }
 #pragma unroll
-                for (int l = 0; l < 5; ++l) m += ab_at(X, k, l, u) * pab[l];
+                for (int l = 0; l < 5; ++l) m = fma(ab_at(X, k, l, u), pab[l], m);
             }
             M[8 * u + w] = m;
         }
@@ -1049,9 +1049,9 @@ __device__ bool factor_par(const Ctx& X) {
             gain(j, kj);
             double a = M[8 * i + j], b = M[8 * j + i];
 #pragma unroll
-            for (int l = 0; l < 3; ++l) a += M[8 * (5 + l) + i] * kj[l];
+            for (int l = 0; l < 3; ++l) a = fma(M[8 * (5 + l) + i], kj[l], a);
 #pragma unroll
-            for (int l = 0; l < 3; ++l) b += M[8 * (5 + l) + j] * ki[l];
+            for (int l = 0; l < 3; ++l) b = fma(M[8 * (5 + l) + j], ki[l], b);
             P[ln] = 0.5 * (a + b);
         }
         sync();

@@ -13,6 +13,9 @@ import torch
 import mpcplan
 import workloads as W
 
+if os.environ.get("PLAN_LIB"):      # A/B of library variants
+    mpcplan.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", os.environ["PLAN_LIB"])
+
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 dev = torch.device("cuda", 0)
 r = W.plan_route("traj3")

@@ -12,6 +12,9 @@ import torch
 import mpcplan
 import workloads as W
 
+if os.environ.get("PLAN_LIB"):      # A/B of library variants (tools/gpu_plan_lib_ab.sh)
+    mpcplan.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", os.environ["PLAN_LIB"])
+
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 route = sys.argv[3] if len(sys.argv) > 3 else "traj1"
 ff = float(sys.argv[4]) if len(sys.argv) > 4 else 0.25
