@@ -50,6 +50,7 @@
 #define AL_STEPS 4            /* refinement + multiplier updates of that solve */
 #define AL_TOL 1e-13        /* stop the refinements once the multiplier update is at rounding level */
 #define POLISH_ROUNDS 6
+#define WARM_ROUNDS 5         /* active-set rounds from the previous QP's classification before the interior point */
 #define SHIFT0 1.0            /* interior-point start: s = max(row, 0) + SHIFT0, lambda = 1 */
 #define TAU 0.995
 #define CYCLE_REL 1e-6
@@ -993,7 +994,7 @@ static int ipm(qp_t* Q, const plan_params* p, qpsol_t* X, int* iters) {
     return rc;
 }
 
-/* one QP: crossover from the previous classification (when given), else interior point + polish.
+/* one QP: active-set rounds from the previous classification (when given), else interior point + polish.
  * Returns 0 solved (exact KKT point), 1 interior-point answer without a certified polish, -1 failure. */
 static int qp_solve(qp_t* Q, const plan_params* p, qpsol_t* X, int have_cls, int* iters) {
     static __thread unsigned char act[MAXNP][NR];
@@ -1007,12 +1008,19 @@ static int qp_solve(qp_t* Q, const plan_params* p, qpsol_t* X, int have_cls, int
         memcpy(act, X->act, sizeof(act));
         for (int k = 0; k <= N; ++k)
             for (int j = 0; j < Q->nr[k]; ++j) lam[k][j] = X->lam[k][j];
-        if (eqp(Q, act, z, lam, nu, scale) == 0) {
-            memcpy(X->z, z, sizeof(double) * NZ * (N + 1));
-            memcpy(X->lam, lam, sizeof(lam));
-            X->nu[0] = nu[0];
-            X->nu[1] = nu[1];
-            return 0;
+        /* each round corrects the rows that contradict the classification (eqp), so a set that moved by a
+         * few rows since the last QP is recovered in a few equality solves instead of a cold interior point */
+        for (int round = 0; round < WARM_ROUNDS; ++round) {
+            const int bad = eqp(Q, act, z, lam, nu, scale);
+            if (bad < 0) break;
+            if (bad == 0) {
+                memcpy(X->z, z, sizeof(double) * NZ * (N + 1));
+                memcpy(X->lam, lam, sizeof(lam));
+                memcpy(X->act, act, sizeof(act));
+                X->nu[0] = nu[0];
+                X->nu[1] = nu[1];
+                return 0;
+            }
         }
     }
     const int rc = ipm(Q, p, X, iters);

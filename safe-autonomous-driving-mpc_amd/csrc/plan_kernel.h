@@ -32,6 +32,7 @@ constexpr double RHO = 1e8;       // penalty of the active rows in the equality-
 constexpr int AL_STEPS = 4;
 constexpr double AL_TOL = 1e-13;   // refinements stop once the multiplier update is at rounding level
 constexpr int POLISH_ROUNDS = 6;
+constexpr int WARM_ROUNDS = 5;      // active-set rounds from the previous QP's classification (oracle qp_solve)
 constexpr double SHIFT0 = 1.0;
 constexpr double TAU = 0.995;
 constexpr double CYCLE_REL = 1e-6;
@@ -1443,9 +1444,13 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
             for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
         }
         sync();
-        if (eqp(X, scale) == 0) {
-            accept_polish(X, false);
-            return 0;
+        for (int round = 0; round < WARM_ROUNDS; ++round) {
+            const int bad = eqp(X, scale);
+            if (bad < 0) break;
+            if (bad == 0) {
+                accept_polish(X, true);
+                return 0;
+            }
         }
     }
     const int rc = ipm(X, iters);

@@ -38,8 +38,10 @@ def kernels():
 
 
 def test_all_solver_instantiations_present(kernels):
-    # GL x OBS x MODE x NT: runtime horizon for GL 16/32/64, NT = 20, 30 (GL 32) and 40 (GL 64)
-    assert len(kernels) == 48
+    # GL x OBS x MODE x NT: runtime horizon for GL 16/32/64, NT = 20, 30 (GL 32) and 40 (GL 64), plus the
+    # GL = 64 interior-point kernels of the N = 20 A/B switch (MPC_IPM_GL64)
+    assert len(kernels) == 50
+    assert (64, 0, 2, 20) in kernels and (64, 1, 2, 20) in kernels
 
 
 def test_c2_path_has_no_scratch(kernels):
