@@ -64,7 +64,7 @@ def main():
                          "optimize_full_trajectory poses them (20 m chunks, per-chunk horizon) on --plan-route; "
                          "reported as 'plan' in chunks/s, never as 'value' (0: skip)")
     ap.add_argument("--plan-steps", type=int, default=3, metavar="K")
-    ap.add_argument("--plan-fleet", type=int, default=0, metavar="B",
+    ap.add_argument("--plan-fleet", type=int, default=1024, metavar="B",
                     help="planner leg, secondary: B full plans on trajectory1's route from random starts, all "
                          "advancing together (trajectory_planning.optimize_full_trajectory_batch), rank 0 only")
     ap.add_argument("--plan-route", default="traj3")
@@ -616,8 +616,9 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
 
 def plan_fleet(B, device):
     """B complete plans of trajectory1's route (the reference's chunk loop, :491-548) from random starts along
-    it, advancing together: one batched launch per round (trajectory_planning.optimize_full_trajectory_batch),
-    wall time including the host loop; the restated checks on every plan."""
+    it (trajectory_planning.optimize_full_trajectory_batch): the loop on the device (plan_optimize_device, each
+    plan on its own wavefront), and for comparison one batched launch per round from the host; wall time
+    including the host bookkeeping; the restated checks on every plan."""
     import numpy as np
     import trajectory_planning as TP
     import workloads as W
@@ -628,16 +629,25 @@ def plan_fleet(B, device):
         s0 = rng.uniform(1.0, r.s_total - 30.0)
         starts[b] = (s0, rng.normal(0, 0.05), rng.normal(0, 0.01), r.k_ref_fun(s0),
                      rng.uniform(0.2, 0.9) * r.v_max_fun(s0))
+    TP.optimize_full_trajectory_batch(r, starts[:4], device=device)          # warm-up (module load, context)
     t0 = time.perf_counter()
     plans, summary = TP.optimize_full_trajectory_batch(r, starts, device=device)
     dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    plans_r, summary_r = TP.optimize_full_trajectory_batch(r, starts, device=device, device_loop=False)
+    dt_r = time.perf_counter() - t0
+    same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(plans, plans_r))
     chunks = sum(len(q["statuses"]) for q in summary)
     return {"plans": B, "seconds": dt, "plans_per_s": B / dt, "chunks": chunks, "chunks_per_s": chunks / dt,
-            "rounds": max(len(q["statuses"]) for q in summary),
+            "max_chunks_per_plan": max(len(q["statuses"]) for q in summary),
             "checks_passed": int(sum(bool(q["passed"]) for q in summary)),
+            "round_loop": {"seconds": dt_r, "plans_per_s": B / dt_r, "identical_plans": bool(same),
+                           "note": "one batched chunk launch per round from the host (device_loop=False): each "
+                                   "round waits for its slowest chunk"},
             "route": f"traj1 ({r.s_total:.0f} m), starts uniform along it (the first the reference's)",
-            "note": "wall time of the whole batched receding-horizon loop (host bookkeeping included); one "
-                    "launch per round over the unfinished plans"}
+            "note": "wall time of the whole receding-horizon loop for every plan, the loop on the device "
+                    "(plan_optimize_device: every plan on its own wavefront, no barrier across plans), plans "
+                    "assembled on the host"}
 
 
 def plan_cpu_baseline(route, wb, budget_s, status, groups):

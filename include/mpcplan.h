@@ -100,6 +100,25 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
                              const double* s_target, const int* is_final, double* X, double* U, double* S,
                              int* status, int* iters, int* sqp, void* stream);
 
+/* The chunk loop of optimize_full_trajectory (trajectory_planning.py:491-548) for B plans, on the device,
+ * asynchronous on `stream`; device pointers.  Replaces the host loop over chunks (:491) for a batch of start
+ * states: each plan advances on its own wavefront, chunk after chunk, with no barrier across plans.
+ *   starts[B][5]        first current_x0 of each plan (:486; the reference's is all zeros)
+ *   max_chunk_size      :419 (20 m); a chunk is final when the remaining distance is < 2 max_chunk_size
+ *   max_chunks          chunks per plan at most (the reference has no cap); also the slot count below
+ *   avg[nav]            avg[i] = mean(vmax[i:]) over the route's speed-limit array (:507, np.mean, which
+ *                       the caller computes so that N matches the host loop bit for bit)
+ *   Nmax                bounds every chunk's N = ceil(size / avg[int(s / 5)] * 2 / 0.3) (:507-515)
+ * Outputs per plan b and chunk slot n < max_chunks (slot = b * max_chunks + n): X[slot][Nmax+1][5],
+ * U[slot][Nmax][2], S[slot][Nmax] (the chunk's whole plan, rows past its N zero), N[slot], is_final[slot],
+ * status[slot], iters[slot], sqp[slot]; nchunks[b] = chunks run, or -(n + 1) when chunk n's N falls outside
+ * [1, Nmax] or int(s / 5) outside avg (the reference raises there).  The committed trajectory is the first
+ * int(N/2) intervals of each non-final chunk and the whole final chunk (:523-541), which the caller
+ * concatenates (trajectory_planning.optimize_full_trajectory_batch).  No scratch memory; capturable. */
+int plan_optimize_device(plan_ctx* c, int B, int Nmax, const double* starts, double max_chunk_size, int max_chunks,
+                         const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final,
+                         int* status, int* iters, int* sqp, int* nchunks, void* stream);
+
 /* Route functions on the device, for tests: kappa(s) and dkappa/ds (k_ref_fun, :445-459), v_max(s). */
 int plan_route_eval(plan_ctx* c, int n, const double* s, double* kappa, double* dkappa, double* vmax);
 

@@ -205,6 +205,49 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
     return PLAN_SUCCESS;
 }
 
+int plan_optimize_device(plan_ctx* c, int B, int Nmax, const double* starts, double max_chunk_size, int max_chunks,
+                         const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final,
+                         int* status, int* iters, int* sqp, int* nchunks, void* stream) {
+    if (!c) return fail(PLAN_E_ARG, "ctx is NULL");
+    if (B < 0) return fail(PLAN_E_ARG, "B must be >= 0");
+    if (B == 0) return PLAN_SUCCESS;
+    if (!starts || !avg || !X || !U || !S || !N || !is_final || !status || !iters || !sqp || !nchunks)
+        return fail(PLAN_E_ARG, "plan_optimize_device: every array is required");
+    if (Nmax < 1 || Nmax > PLAN_MAX_N) return fail(PLAN_E_ARG, "Nmax out of range [1, PLAN_MAX_N]");
+    if (max_chunks < 1) return fail(PLAN_E_ARG, "max_chunks must be >= 1");
+    if (nav < 1) return fail(PLAN_E_ARG, "avg must have at least one entry");
+    if (!(max_chunk_size > 0.0) || !std::isfinite(max_chunk_size)) return fail(PLAN_E_ARG, "max_chunk_size must be > 0");
+    const size_t lds = lds_bytes(Nmax);
+    if (lds > c->lds_max) return fail(PLAN_E_ARG, "Nmax too large for the device's LDS");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");
+    if (lds > 65536 &&
+        hipFuncSetAttribute((const void*)plan_loop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(PLAN_E_LAUNCH, "cannot raise the kernel's LDS limit");
+    LArgs a;
+    a.R = c->R;
+    a.P = c->p;
+    a.B = B;
+    a.Nmax = Nmax;
+    a.max_chunks = max_chunks;
+    a.nav = nav;
+    a.max_chunk_size = max_chunk_size;
+    a.avg = avg;
+    a.starts = starts;
+    a.X = X;
+    a.U = U;
+    a.S = S;
+    a.N = N;
+    a.fin = is_final;
+    a.status = status;
+    a.iters = iters;
+    a.sqp = sqp;
+    a.nchunks = nchunks;
+    hipLaunchKernelGGL(plan_loop_kernel, dim3(B), dim3(WAVE), lds, (hipStream_t)stream, a);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess)
+        return fail(PLAN_E_LAUNCH, std::string("plan loop kernel launch failed: ") + hipGetErrorString(e));
+    return PLAN_SUCCESS;
+}
+
 int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const double* s_target, const int* is_final,
                       double* X, double* U, double* S, int* status, int* iters, int* sqp) {
     if (!c) return fail(PLAN_E_ARG, "ctx is NULL");

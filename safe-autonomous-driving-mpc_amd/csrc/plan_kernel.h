@@ -1622,60 +1622,13 @@ __device__ double cost_dir(const Ctx& X) {
 
 __device__ inline ldsd* lds_p(const Ctx& X) { return X.L; }
 
-struct KArgs {
-    DevRoute R;
-    plan_params P;
-    int B, Nmax, Nfixed, dbg;
-    const int* N;
-    const double *x0, *st;
-    const int* fin;
-    double *X, *U, *S;
-    int *status, *iters, *sqp;
-};
-
-__global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
-    PLAN_LDS_DECL;
-    const int b = blockIdx.x;
-    Ctx X;
-    X.R = a.R;
-    X.P = a.P;
-    X.Y = make_layout(a.Nmax);
-    X.L = (ldsd*)lds;
-    X.ln = threadIdx.x;
-    X.dbg = a.dbg;
-    X.N = a.N ? a.N[b] : a.Nfixed;
-    if (X.N < 1 || X.N > a.Nmax) {
-        // a per-chunk horizon outside [1, Nmax] (device arrays are not validated on the host): no solve, zero
-        // plan, status PLAN_NUMERICAL (the chunk's LDS block is sized for Nmax)
-        for (int k = threadIdx.x; k <= a.Nmax; k += WAVE) {
-            if (a.X)
-                for (int i = 0; i < 5; ++i) a.X[((size_t)b * (a.Nmax + 1) + k) * 5 + i] = 0.0;
-            if (k < a.Nmax) {
-                if (a.U) a.U[((size_t)b * a.Nmax + k) * 2] = a.U[((size_t)b * a.Nmax + k) * 2 + 1] = 0.0;
-                if (a.S) a.S[(size_t)b * a.Nmax + k] = 0.0;
-            }
-        }
-        if (threadIdx.x == 0) {
-            if (a.status) a.status[b] = PLAN_NUMERICAL;
-            if (a.iters) a.iters[b] = 0;
-            if (a.sqp) a.sqp[b] = 0;
-        }
-        return;
-    }
+// one chunk NLP (trajectory_planning.py:351-390) at X.x0, X.st, X.fin, X.N, set by the caller: the plan is
+// left in the LDS block (ZB); returns the status, the interior-point iterations and QPs in *total_out, *nq_out
+__device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) {
     const int N = X.N;
-    X.fin = a.fin ? (a.fin[b] != 0) : 0;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) X.x0[i] = a.x0[5 * (size_t)b + i];
-    X.st = a.st[b];
-    X.den = fmax(1.0, a.R.s_total - X.x0[0]);
+    X.den = fmax(1.0, X.R.s_total - X.x0[0]);
     X.nu[0] = X.nu[1] = 0.0;
     X.delta = 0.0;
-#ifdef PLAN_PROF
-    if (X.ln == 0)
-        for (int i = 0; i < 16; ++i) *(PLAN_LDS_AS unsigned long long*)(lds_p(X) + X.Y.oSC + 16 + i) = 0ull;
-    sync();
-    const unsigned long long t_total0 = __builtin_amdgcn_s_memtime();
-#endif
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     // initial guess (:357-376)
@@ -1693,7 +1646,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
     bool have_cls = false, frozen = false;
     double last = INFINITY, mu_m = 0.0, hf[LS_MEMORY], hv[LS_MEMORY];
     int nh = 0;
-    for (int it = 0; it < a.P.sqp_iters; ++it, ++since) {
+    for (int it = 0; it < X.P.sqp_iters; ++it, ++since) {
         bool exact = last <= EXACT_STEP;
         int rc = -1;
         for (;;) {
@@ -1774,7 +1727,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
             }
         sync();
         last = step;
-        if (step <= a.P.sqp_tol) { status = frozen ? PLAN_FROZEN_LIMITS : PLAN_OK; break; }
+        if (step <= X.P.sqp_tol) { status = frozen ? PLAN_FROZEN_LIMITS : PLAN_OK; break; }
         if (since >= 2 && back2 <= CYCLE_REL * step) {
             if (frozen) break;
             for (int k = X.ln; k <= N; k += WAVE)
@@ -1794,6 +1747,66 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
                 bad = 1.0;
         if (wmax(bad) > 0.0) status = PLAN_NOT_CONVERGED;
     }
+    *total_out = total;
+    *nq_out = nq;
+    return status;
+}
+
+struct KArgs {
+    DevRoute R;
+    plan_params P;
+    int B, Nmax, Nfixed, dbg;
+    const int* N;
+    const double *x0, *st;
+    const int* fin;
+    double *X, *U, *S;
+    int *status, *iters, *sqp;
+};
+
+__global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
+    PLAN_LDS_DECL;
+    const int b = blockIdx.x;
+    Ctx X;
+    X.R = a.R;
+    X.P = a.P;
+    X.Y = make_layout(a.Nmax);
+    X.L = (ldsd*)lds;
+    X.ln = threadIdx.x;
+    X.dbg = a.dbg;
+    X.N = a.N ? a.N[b] : a.Nfixed;
+    if (X.N < 1 || X.N > a.Nmax) {
+        // a per-chunk horizon outside [1, Nmax] (device arrays are not validated on the host): no solve, zero
+        // plan, status PLAN_NUMERICAL (the chunk's LDS block is sized for Nmax)
+        for (int k = threadIdx.x; k <= a.Nmax; k += WAVE) {
+            if (a.X)
+                for (int i = 0; i < 5; ++i) a.X[((size_t)b * (a.Nmax + 1) + k) * 5 + i] = 0.0;
+            if (k < a.Nmax) {
+                if (a.U) a.U[((size_t)b * a.Nmax + k) * 2] = a.U[((size_t)b * a.Nmax + k) * 2 + 1] = 0.0;
+                if (a.S) a.S[(size_t)b * a.Nmax + k] = 0.0;
+            }
+        }
+        if (threadIdx.x == 0) {
+            if (a.status) a.status[b] = PLAN_NUMERICAL;
+            if (a.iters) a.iters[b] = 0;
+            if (a.sqp) a.sqp[b] = 0;
+        }
+        return;
+    }
+    const int N = X.N;
+    X.fin = a.fin ? (a.fin[b] != 0) : 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) X.x0[i] = a.x0[5 * (size_t)b + i];
+    X.st = a.st[b];
+#ifdef PLAN_PROF
+    if (X.ln == 0)
+        for (int i = 0; i < 16; ++i) *(PLAN_LDS_AS unsigned long long*)(lds_p(X) + X.Y.oSC + 16 + i) = 0ull;
+    sync();
+    const unsigned long long t_total0 = __builtin_amdgcn_s_memtime();
+#endif
+    int total = 0, nq = 0;
+    const int status = solve_chunk(X, &total, &nq);
+    ldsd* L = X.L;
+    const Layout& Y = X.Y;
     // outputs: rows past this chunk's N are zero
     const int Nm = a.Nmax;
     for (int k = X.ln; k <= Nm; k += WAVE) {
@@ -1821,6 +1834,87 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         atomicAdd(&g_plan_prof[15], 1ull);
     }
 #endif
+}
+
+// The receding-horizon loop of optimize_full_trajectory (trajectory_planning.py:491-548) on the device: wave
+// b runs plan b's chunks one after another from starts[b], with no barrier across plans (a launch over B plans
+// lasts as long as the slowest plan's chain of chunks, not the sum over rounds of each round's slowest chunk).
+// Chunk n of plan b: remaining = s_total - s; final when remaining < 2 max_chunk_size (size = remaining, else
+// max_chunk_size); N = ceil(size / avg[int(s / 5)] * 2 / 0.3) with avg[i] = mean(vmax[i:]) (the reference's
+// np.mean over the speed-limit array, :507, computed by the caller); the chunk's plan, horizon, final flag and
+// status go to slot (b, n); the next start is X[N/2] (the reference's commit of the first int(N/2)
+// intervals, :523-541) or X[N] after a final chunk.  The loop ends when remaining <= 0.1 or after
+// max_chunks chunks; nchunks[b] = chunks run, or -(n + 1) when chunk n's horizon is outside [1, Nmax] (or
+// int(s / 5) outside avg), the reference's ValueError.
+struct LArgs {
+    DevRoute R;
+    plan_params P;
+    int B, Nmax, max_chunks, nav;
+    double max_chunk_size;
+    const double* avg;
+    const double* starts;
+    double *X, *U, *S;
+    int *N, *fin, *status, *iters, *sqp, *nchunks;
+};
+
+__global__ void __launch_bounds__(WAVE) plan_loop_kernel(LArgs a) {
+    PLAN_LDS_DECL;
+    const int b = blockIdx.x;
+    Ctx X;
+    X.R = a.R;
+    X.P = a.P;
+    X.Y = make_layout(a.Nmax);
+    X.L = (ldsd*)lds;
+    X.ln = threadIdx.x;
+    X.dbg = 0;
+    const Layout& Y = X.Y;
+    const int Nm = a.Nmax;
+    double x0[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) x0[i] = a.starts[5 * (size_t)b + i];
+    int n = 0;
+    bool err = false;
+    for (; n < a.max_chunks; ++n) {
+        const double rem = a.R.s_total - x0[0];
+        if (!(rem > 0.1)) break;
+        const int fin = rem < a.max_chunk_size * 2.0 ? 1 : 0;
+        const double size = fin ? rem : a.max_chunk_size;
+        const double si = x0[0] / 5.0;
+        if (!(si > -1.0) || !(si < (double)a.nav)) { err = true; break; }
+        const double hz = ceil(size / a.avg[(int)si] * 2.0 / 0.3);
+        if (!(hz >= 1.0 && hz <= (double)Nm)) { err = true; break; }
+        X.N = (int)hz;
+        X.fin = fin;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) X.x0[i] = x0[i];
+        X.st = x0[0] + size;
+        int total = 0, nq = 0;
+        const int status = solve_chunk(X, &total, &nq);
+        const int N = X.N;
+        const size_t slot = (size_t)b * a.max_chunks + n;
+        ldsd* L = X.L;
+        for (int k = X.ln; k <= Nm; k += WAVE) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) a.X[(slot * (Nm + 1) + k) * 5 + i] = k <= N ? L[Y.oZB + ZS * k + i] : 0.0;
+            if (k < Nm) {
+                a.U[(slot * Nm + k) * 2 + 0] = k < N ? L[Y.oZB + ZS * k + 5] : 0.0;
+                a.U[(slot * Nm + k) * 2 + 1] = k < N ? L[Y.oZB + ZS * k + 6] : 0.0;
+                a.S[slot * Nm + k] = k < N ? L[Y.oZB + ZS * k + 7] : 0.0;
+            }
+        }
+        if (X.ln == 0) {
+            a.N[slot] = N;
+            a.fin[slot] = fin;
+            a.status[slot] = status;
+            a.iters[slot] = total;
+            a.sqp[slot] = nq;
+        }
+        const int c = fin ? N : N / 2;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x0[i] = L[Y.oZB + ZS * c + i];
+        sync();          // every lane has its next start before the next chunk rewrites the block
+    }
+    if (X.ln == 0) a.nchunks[b] = err ? -(n + 1) : n;
 }
 
 __global__ void route_eval_kernel(DevRoute R, int n, const double* s, double* k, double* dk, double* vm) {

@@ -32,8 +32,8 @@ class PlanError(RuntimeError):
     pass
 
 
-EXPORTS = ["plan_default_params", "plan_create", "plan_solve_chunks", "plan_solve_chunks_device", "plan_route_eval",
-           "plan_set_params", "plan_last_error", "plan_version", "plan_destroy"]
+EXPORTS = ["plan_default_params", "plan_create", "plan_solve_chunks", "plan_solve_chunks_device", "plan_optimize_device",
+           "plan_route_eval", "plan_set_params", "plan_last_error", "plan_version", "plan_destroy"]
 
 _lib = None
 
@@ -53,6 +53,9 @@ def lib():
     L.plan_solve_chunks.argtypes = [C.c_void_p, C.c_int, _ip, _dp, _dp, _ip, _dp, _dp, _dp, _ip, _ip, _ip]
     L.plan_solve_chunks_device.restype = C.c_int
     L.plan_solve_chunks_device.argtypes = [C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 11
+    L.plan_optimize_device.restype = C.c_int
+    L.plan_optimize_device.argtypes = ([C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_double, C.c_int, C.c_void_p,
+                                        C.c_int] + [C.c_void_p] * 10)
     L.plan_route_eval.restype = C.c_int
     L.plan_route_eval.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]
     L.plan_set_params.restype = C.c_int
@@ -141,6 +144,33 @@ class Planner:
                                               X_ptr or None, U_ptr or None, S_ptr or None, status_ptr or None,
                                               iters_ptr or None, sqp_ptr or None, C.c_void_p(stream)),
                "plan_solve_chunks_device")
+
+    def optimize_device(self, starts, max_chunk_size, max_chunks, avg, Nmax, device=0):
+        """plan_optimize_device (include/mpcplan.h): the chunk loop of optimize_full_trajectory for B plans on
+        the device, up to max_chunks chunks each.  starts [B,5]; avg [nav] = mean(vmax[i:]).  Returns dict of
+        numpy arrays: X [B,C,Nmax+1,5], U [B,C,Nmax,2], S [B,C,Nmax], N, is_final, status, iters, sqp [B,C]
+        (C = max_chunks slots) and nchunks [B]."""
+        import torch
+        dev = torch.device("cuda", device)
+        starts = np.ascontiguousarray(starts, np.float64).reshape(-1, 5)
+        B, Cn = starts.shape[0], int(max_chunks)
+        f64 = dict(dtype=torch.float64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        d_st = torch.as_tensor(starts, **f64).contiguous()
+        d_avg = torch.as_tensor(np.ascontiguousarray(avg, np.float64), **f64).contiguous()
+        out = dict(X=torch.zeros((B, Cn, Nmax + 1, 5), **f64), U=torch.zeros((B, Cn, Nmax, 2), **f64),
+                   S=torch.zeros((B, Cn, Nmax), **f64))
+        for k in ("N", "is_final", "status", "iters", "sqp"):
+            out[k] = torch.zeros((B, Cn), **i32)
+        out["nchunks"] = torch.zeros(B, **i32)
+        stream = torch.cuda.current_stream(dev)
+        _check(lib().plan_optimize_device(self.h, B, int(Nmax), d_st.data_ptr(), float(max_chunk_size), Cn,
+                                          d_avg.data_ptr(), int(d_avg.numel()),
+                                          *[out[k].data_ptr() for k in ("X", "U", "S", "N", "is_final", "status",
+                                                                        "iters", "sqp", "nchunks")],
+                                          C.c_void_p(stream.cuda_stream)), "plan_optimize_device")
+        torch.cuda.synchronize(dev)
+        return {k: v.cpu().numpy() for k, v in out.items()}
 
     def route_eval(self, s):
         """kappa(s), d kappa / ds and v_max(s) on the device (k_ref_fun / v_max_fun)."""

@@ -174,7 +174,54 @@ def optimize_full_trajectory(route, max_chunk_size=20, max_chunks=10000, device=
     return X_final, U_final, S_final
 
 
-def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=10000, device=0, solve_chunks=None):
+def _commit(pieces, X, U, S, n, fin):
+    """:523-541: the first int(N/2) intervals of a non-final chunk, the whole final chunk; returns the next start."""
+    if not fin:
+        c = int(n / 2)
+        pieces.append((X[:c + 1] if not pieces else X[1:c + 1], U[:c], S[:c]))
+    else:
+        pieces.append((X[1:], U, S))
+    return pieces[-1][0][-1]
+
+
+def _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, statuses, horizons, opt, seg=64):
+    """optimize_full_trajectory_batch's chunk loop as plan_optimize_device launches: every plan advances on its
+    own wavefront, up to `seg` chunks per launch (plans still running continue from their last start)."""
+    s_total = route.s_total
+    vm = np.asarray(route.vmax, np.float64)
+    avg = np.array([float(np.mean(vm[i:])) for i in range(vm.size)])     # route.avg_speed_from(5 i), :507
+    nb = int(np.max(np.ceil(2.0 * max_chunk_size / avg * 2.0 / 0.3)))
+    Nmax = min(max(nb, 1), mpcplan.PLAN_MAX_N)
+    opt.N, opt.dt = Nmax, 0.3
+    pl = mpcplan.Planner(route, opt.params(0.0), device=device)
+    try:
+        cur = np.asarray(starts, np.float64).copy()
+        act = np.arange(cur.shape[0])
+        used = 0
+        while act.size and used < max_chunks:
+            C_ = min(seg, max_chunks - used)
+            r = pl.optimize_device(cur[act], max_chunk_size, C_, avg, Nmax, device=device)
+            nxt = []
+            for i, b in enumerate(act):
+                nc = int(r["nchunks"][i])
+                for j in range(abs(nc) - (1 if nc < 0 else 0)):
+                    n, fin = int(r["N"][i, j]), int(r["is_final"][i, j])
+                    statuses[b].append(int(r["status"][i, j]))
+                    horizons[b].append(n)
+                    cur[b] = _commit(pieces[b], r["X"][i, j, :n + 1], r["U"][i, j, :n], r["S"][i, j, :n], n, fin)
+                if nc < 0:
+                    raise ValueError(f"chunk horizon of plan {b} exceeds PLAN_MAX_N={mpcplan.PLAN_MAX_N} (or its "
+                                     f"start lies outside the route)")
+                if nc == C_ and s_total - cur[b, 0] > 0.1:
+                    nxt.append(b)
+            used += C_
+            act = np.array(nxt, dtype=int)
+    finally:
+        pl.close()
+
+
+def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=10000, device=0, solve_chunks=None,
+                                   device_loop=True):
     """The chunk loop of optimize_full_trajectory (trajectory_planning.py:491-548) for B plans on one route at
     once, from B start states (e.g. a fleet re-planning from where each vehicle is): every round solves the
     current chunk of each unfinished plan in one batched call, each chunk with its own horizon (the
@@ -183,7 +230,10 @@ def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=
 
     Returns (plans, summary): plans[b] = (X, U, S); summary[b] = sanity_checks.plan_check_summary of the plan
     plus 'statuses' and 'horizons' of its chunks.  solve_chunks(x0 [n,5], s_target [n], is_final [n], N [n])
-    -> dict(X, U, S, status) replaces the GPU batch (tests drive this loop with the CPU oracle)."""
+    -> dict(X, U, S, status) replaces the GPU batch (tests drive this loop with the CPU oracle).
+    device_loop (GPU, the default): the whole loop runs on the device (plan_optimize_device), each plan on its
+    own wavefront with no barrier across plans; False: one batched chunk launch per round, the host loop
+    below.  Both give the same plans bit for bit (the same chunk solver on the same chunk inputs)."""
     from sanity_checks import plan_check_summary
     if isinstance(route, dict):
         import routes
@@ -198,6 +248,9 @@ def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=
     done = np.zeros(B, bool)
     opt = TrajectoryOptimizer(device=device)
     pl = None
+    if solve_chunks is None and device_loop:
+        _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, statuses, horizons, opt)
+        max_chunks = 0                                                 # the host loop below does not run
     for _ in range(max_chunks):
         act = np.flatnonzero(~done & (s_total - cur[:, 0] > 0.1))
         done[~done & (s_total - cur[:, 0] <= 0.1)] = True
@@ -223,12 +276,7 @@ def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=
             X, U, S = r["X"][i, :n + 1], r["U"][i, :n], r["S"][i, :n]
             statuses[b].append(int(r["status"][i]))
             horizons[b].append(n)
-            if not fin[i]:                                              # :523-541
-                c = int(n / 2)
-                pieces[b].append((X[:c + 1] if not pieces[b] else X[1:c + 1], U[:c], S[:c]))
-            else:
-                pieces[b].append((X[1:], U, S))
-            cur[b] = pieces[b][-1][0][-1]
+            cur[b] = _commit(pieces[b], X, U, S, n, fin[i])
     if pl is not None:
         pl.close()
     plans, summary = [], []

@@ -196,3 +196,40 @@ def test_batched_receding_loop_on_gpu(env, capsys):
           f"{min(len(q['statuses']) for q in summary)}-{max(len(q['statuses']) for q in summary)}")
     assert passed.mean() >= 0.9
     assert all(abs(p[0][-1, 0] - r.s_total) < 1e-3 for p in plans)
+
+
+@pytest.mark.gpu
+def test_device_loop_equals_round_loop(env, capsys):
+    """plan_optimize_device (each plan's chunk loop on its own wavefront) gives the round-by-round host loop's
+    plans bit for bit: the same chunk solver on the same chunk inputs (start, target, final flag, N).  Also with
+    the loop cut into launches of 2 chunks (plans continue from their last start), and max_chunks honoured."""
+    mpcplan, PO, W = env
+    import trajectory_planning as TP
+    r = W.plan_route("traj1")
+    rng = np.random.default_rng(11)
+    starts = np.zeros((40, 5))
+    for b in range(1, 40):
+        s0 = rng.uniform(1.0, r.s_total - 30.0)
+        starts[b] = (s0, rng.normal(0, 0.05), rng.normal(0, 0.01), r.k_ref_fun(s0), rng.uniform(0.2, 0.9) * r.v_max_fun(s0))
+    pd, sd = TP.optimize_full_trajectory_batch(r, starts, device_loop=True)
+    ph, sh = TP.optimize_full_trajectory_batch(r, starts, device_loop=False)
+    for b in range(40):
+        assert sd[b]["statuses"] == sh[b]["statuses"] and sd[b]["horizons"] == sh[b]["horizons"]
+        for i in range(3):
+            assert np.array_equal(pd[b][i], ph[b][i]), (b, i)
+    # launches of 2 chunks each
+    opt = TP.TrajectoryOptimizer()
+    pieces, st, hz = [[] for _ in range(40)], [[] for _ in range(40)], [[] for _ in range(40)]
+    TP._device_loop(r, starts, 20, 10000, 0, pieces, st, hz, opt, seg=2)
+    for b in range(40):
+        assert st[b] == sd[b]["statuses"] and hz[b] == sd[b]["horizons"]
+        assert np.array_equal(np.concatenate([p[0] for p in pieces[b]]), pd[b][0])
+    # max_chunks caps every plan, as in the host loop
+    pc, sc = TP.optimize_full_trajectory_batch(r, starts, max_chunks=3)
+    pc2, sc2 = TP.optimize_full_trajectory_batch(r, starts, max_chunks=3, device_loop=False)
+    assert all(len(q["statuses"]) <= 3 for q in sc)
+    for b in range(40):
+        assert np.array_equal(pc[b][0], pc2[b][0])
+    with capsys.disabled():
+        print(f"\ndevice loop = round loop on 40 plans, chunks per plan "
+              f"{min(len(q['statuses']) for q in sd)}-{max(len(q['statuses']) for q in sd)}")

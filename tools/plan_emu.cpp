@@ -21,6 +21,7 @@ using std::isfinite;
 #define __device__
 #define __host__
 #define __global__
+#define __forceinline__ inline
 #define __launch_bounds__(x)
 #define __shared__
 
