@@ -112,7 +112,8 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
  * Outputs per plan b and chunk slot n < max_chunks (slot = b * max_chunks + n): X[slot][Nmax+1][5],
  * U[slot][Nmax][2], S[slot][Nmax] (the chunk's whole plan, rows past its N zero), N[slot], is_final[slot],
  * status[slot], iters[slot], sqp[slot]; nchunks[b] = chunks run, or -(n + 1) when chunk n's N falls outside
- * [1, Nmax] or int(s / 5) outside avg (the reference raises there).  The committed trajectory is the first
+ * [1, Nmax] or int(s / 5) past the end of avg (the reference raises there; a negative index counts from the
+ * end, as a Python slice does).  The committed trajectory is the first
  * int(N/2) intervals of each non-final chunk and the whole final chunk (:523-541), which the caller
  * concatenates (trajectory_planning.optimize_full_trajectory_batch).  No scratch memory; capturable. */
 int plan_optimize_device(plan_ctx* c, int B, int Nmax, const double* starts, double max_chunk_size, int max_chunks,

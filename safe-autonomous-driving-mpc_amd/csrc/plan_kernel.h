@@ -1845,7 +1845,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
 // status go to slot (b, n); the next start is X[N/2] (the reference's commit of the first int(N/2)
 // intervals, :523-541) or X[N] after a final chunk.  The loop ends when remaining <= 0.1 or after
 // max_chunks chunks; nchunks[b] = chunks run, or -(n + 1) when chunk n's horizon is outside [1, Nmax] (or
-// int(s / 5) outside avg), the reference's ValueError.
+// int(s / 5) past the end of avg), the reference's ValueError.
 struct LArgs {
     DevRoute R;
     plan_params P;
@@ -1879,9 +1879,13 @@ __global__ void __launch_bounds__(WAVE) plan_loop_kernel(LArgs a) {
         if (!(rem > 0.1)) break;
         const int fin = rem < a.max_chunk_size * 2.0 ? 1 : 0;
         const double size = fin ? rem : a.max_chunk_size;
+        // vmax[int(s / 5):] with Python's slice rules: truncation toward zero, a negative index counts from the
+        // end (clamped at the start), an index past the end leaves an empty slice (nan: the reference raises)
         const double si = x0[0] / 5.0;
-        if (!(si > -1.0) || !(si < (double)a.nav)) { err = true; break; }
-        const double hz = ceil(size / a.avg[(int)si] * 2.0 / 0.3);
+        if (!(si < (double)a.nav)) { err = true; break; }
+        int idx = si <= -(double)a.nav ? 0 : (int)si;
+        if (idx < 0) idx += a.nav;
+        const double hz = ceil(size / a.avg[idx] * 2.0 / 0.3);
         if (!(hz >= 1.0 && hz <= (double)Nm)) { err = true; break; }
         X.N = (int)hz;
         X.fin = fin;

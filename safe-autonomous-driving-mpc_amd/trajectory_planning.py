@@ -211,7 +211,7 @@ def _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, stat
                     cur[b] = _commit(pieces[b], r["X"][i, j, :n + 1], r["U"][i, j, :n], r["S"][i, j, :n], n, fin)
                 if nc < 0:
                     raise ValueError(f"chunk horizon of plan {b} exceeds PLAN_MAX_N={mpcplan.PLAN_MAX_N} (or its "
-                                     f"start lies outside the route)")
+                                     f"start lies past the end of the route)")
                 if nc == C_ and s_total - cur[b, 0] > 0.1:
                     nxt.append(b)
             used += C_

@@ -211,7 +211,11 @@ def test_device_loop_equals_round_loop(env, capsys):
     for b in range(1, 40):
         s0 = rng.uniform(1.0, r.s_total - 30.0)
         starts[b] = (s0, rng.normal(0, 0.05), rng.normal(0, 0.01), r.k_ref_fun(s0), rng.uniform(0.2, 0.9) * r.v_max_fun(s0))
+    starts[1, 0] = -12.0                 # before the route: vmax[int(s / 5):] counts from the end, as in Python
+    starts[2, 0] = -5.0 * len(r.vmax) - 10.0    # int(s / 5) before -len: the whole array, avg[0]
+    starts[3, 0] = r.s_total - 0.05      # already there: no chunk
     pd, sd = TP.optimize_full_trajectory_batch(r, starts, device_loop=True)
+    assert sd[3]["statuses"] == []
     ph, sh = TP.optimize_full_trajectory_batch(r, starts, device_loop=False)
     for b in range(40):
         assert sd[b]["statuses"] == sh[b]["statuses"] and sd[b]["horizons"] == sh[b]["horizons"]
@@ -223,7 +227,8 @@ def test_device_loop_equals_round_loop(env, capsys):
     TP._device_loop(r, starts, 20, 10000, 0, pieces, st, hz, opt, seg=2)
     for b in range(40):
         assert st[b] == sd[b]["statuses"] and hz[b] == sd[b]["horizons"]
-        assert np.array_equal(np.concatenate([p[0] for p in pieces[b]]), pd[b][0])
+        if pieces[b]:
+            assert np.array_equal(np.concatenate([p[0] for p in pieces[b]]), pd[b][0])
     # max_chunks caps every plan, as in the host loop
     pc, sc = TP.optimize_full_trajectory_batch(r, starts, max_chunks=3)
     pc2, sc2 = TP.optimize_full_trajectory_batch(r, starts, max_chunks=3, device_loop=False)
