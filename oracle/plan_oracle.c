@@ -51,6 +51,9 @@
 #define AL_TOL 1e-13        /* stop the refinements once the multiplier update is at rounding level */
 #define POLISH_ROUNDS 6
 #define WARM_ROUNDS 5         /* active-set rounds from the previous QP's classification before the interior point */
+#define MU_CHECK 1e-4         /* interior-point checkpoint: a polish is tried once mu and phi are below this ... */
+#define CHECK_SEP 100.0       /* ... and every row's s and lambda differ by this factor (no near-tie to classify) */
+#define CHECK_ROUNDS 2        /* polish rounds at the checkpoint (the interior point resumes if they fail) */
 #define SHIFT0 1.0            /* interior-point start: s = max(row, 0) + SHIFT0, lambda = 1 */
 #define TAU 0.995
 #define CYCLE_REL 1e-6
@@ -900,23 +903,27 @@ static int eqp(qp_t* Q, unsigned char act[][NR], double z[][NZ], double lam[][NR
     return bad;
 }
 
-/* Mehrotra predictor-corrector interior point on the QP; returns 0 converged, 1 iteration cap, -1 breakdown */
-static int ipm(qp_t* Q, const plan_params* p, qpsol_t* X, int* iters) {
+/* Mehrotra predictor-corrector interior point on the QP; returns 0 converged, 1 iteration cap, -1 breakdown,
+ * 2 checkpoint (first call only: mu and phi below MU_CHECK with every row's s and lambda CHECK_SEP apart).
+ * resume = 1 continues from X, *iters and *phi_io. */
+static int ipm(qp_t* Q, const plan_params* p, qpsol_t* X, int* iters, int resume, double* phi_io) {
     static __thread fac_t F;
     static __thread double W[MAXNP][NR], gl[MAXNP][NZ], dz[MAXNP][NZ], dsa[MAXNP][NR], dla[MAXNP][NR],
         rp[MAXNP][NR], ds[MAXNP][NR], dl[MAXNP][NR];
     const int N = Q->N;
     int m = 0;
-    rollout(Q, X->z);
+    if (!resume) rollout(Q, X->z);
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < Q->nr[k]; ++j) {
-            const double rv = row_val(Q, k, j, X->z[k]);
-            X->s[k][j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
-            X->lam[k][j] = 1.0;
+            if (!resume) {
+                const double rv = row_val(Q, k, j, X->z[k]);
+                X->s[k][j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
+                X->lam[k][j] = 1.0;
+            }
             ++m;
         }
-    double phi = 1.0;
-    int it = 0, rc = 1;
+    double phi = resume ? *phi_io : 1.0;
+    int it = resume ? *iters : 0, rc = 1;
     for (; it < p->max_iter; ++it) {
         double mu = 0.0;
         for (int k = 0; k <= N; ++k)
@@ -927,6 +934,15 @@ static int ipm(qp_t* Q, const plan_params* p, qpsol_t* X, int* iters) {
         mu /= m;
         if (!isfinite(mu)) { rc = -1; break; }
         if (mu <= p->tol && phi <= 1e-12) { rc = 0; break; }
+        if (!resume && mu <= MU_CHECK && phi <= MU_CHECK) {
+            int tie = 0;
+            for (int k = 0; k <= N; ++k)
+                for (int j = 0; j < Q->nr[k]; ++j) {
+                    const double s = X->s[k][j], l = X->lam[k][j];
+                    if (!(s > CHECK_SEP * l || l > CHECK_SEP * s)) tie = 1;
+                }
+            if (!tie) { rc = 2; break; }
+        }
         for (int k = 0; k <= N; ++k)
             for (int j = 0; j < Q->nr[k]; ++j) W[k][j] = X->lam[k][j] / X->s[k][j];
         if (factor_reg(Q, (const double(*)[NR])W, &F)) { rc = -1; break; }
@@ -991,6 +1007,7 @@ static int ipm(qp_t* Q, const plan_params* p, qpsol_t* X, int* iters) {
         phi *= 1.0 - alpha;
     }
     *iters = it;
+    *phi_io = phi;
     return rc;
 }
 
@@ -1023,7 +1040,30 @@ static int qp_solve(qp_t* Q, const plan_params* p, qpsol_t* X, int have_cls, int
             }
         }
     }
-    const int rc = ipm(Q, p, X, iters);
+    double phi = 1.0;
+    int rc = ipm(Q, p, X, iters, 0, &phi);
+    if (rc == 2) {
+        /* checkpoint: the loose interior point's classification (no near-ties) is often already the
+         * optimum's, which the polish then certifies exactly; otherwise the interior point resumes */
+        for (int k = 0; k <= N; ++k)
+            for (int j = 0; j < Q->nr[k]; ++j) {
+                act[k][j] = X->s[k][j] < X->lam[k][j];
+                lam[k][j] = X->lam[k][j];
+            }
+        for (int round = 0; round < CHECK_ROUNDS; ++round) {
+            const int bad = eqp(Q, act, z, lam, nu, scale);
+            if (bad < 0) break;
+            if (bad == 0) {
+                memcpy(X->z, z, sizeof(double) * NZ * (N + 1));
+                memcpy(X->lam, lam, sizeof(lam));
+                memcpy(X->act, act, sizeof(act));
+                X->nu[0] = nu[0];
+                X->nu[1] = nu[1];
+                return 0;
+            }
+        }
+        rc = ipm(Q, p, X, iters, 1, &phi);
+    }
     if (rc < 0) return -1;
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < Q->nr[k]; ++j) {

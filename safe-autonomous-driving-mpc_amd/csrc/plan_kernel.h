@@ -33,6 +33,9 @@ constexpr int AL_STEPS = 4;
 constexpr double AL_TOL = 1e-13;   // refinements stop once the multiplier update is at rounding level
 constexpr int POLISH_ROUNDS = 6;
 constexpr int WARM_ROUNDS = 5;      // active-set rounds from the previous QP's classification (oracle qp_solve)
+constexpr double MU_CHECK = 1e-4;   // interior-point checkpoint: a polish is tried once mu and phi are below this ...
+constexpr double CHECK_SEP = 100.0; // ... and every row's s and lambda differ by this factor (no near-tie)
+constexpr int CHECK_ROUNDS = 2;     // polish rounds at the checkpoint (the interior point resumes if they fail)
 constexpr double SHIFT0 = 1.0;
 constexpr double TAU = 0.995;
 constexpr double CYCLE_REL = 1e-6;
@@ -1263,13 +1266,15 @@ __device__ int eqp(Ctx& X, double scale) {
     return bad;
 }
 
-// Mehrotra predictor-corrector interior point; solution in Z, S, LAM; 0 converged, 1 cap, -1 breakdown
-__device__ int ipm(Ctx& X, int* iters) {
+// Mehrotra predictor-corrector interior point; solution in Z, S, LAM; 0 converged, 1 cap, -1 breakdown, 2
+// checkpoint (first call only: mu and phi below MU_CHECK, every row's s and lambda CHECK_SEP apart); resume
+// continues from Z, S, LAM, *iters, *phi_io (oracle ipm)
+__device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     PHASE(PH_IPM);
     const int N = X.N;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
-    rollout(X, Y.oZ);
+    if (!resume) rollout(X, Y.oZ);
     int m = 0;
     for (int k = X.ln; k <= N; k += WAVE) {
         double z[NZ];
@@ -1277,16 +1282,18 @@ __device__ int ipm(Ctx& X, int* iters) {
         for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         for_rows(k, N, X.fin, [&](int kind, int j) {
-            const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
-            L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
-            L[Y.oLAM + NR * k + j] = 1.0;
+            if (!resume) {
+                const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
+                L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
+                L[Y.oLAM + NR * k + j] = 1.0;
+            }
             ++m;
         });
     }
     m = wsumi(m);
     sync();
-    double phi = 1.0;
-    int it = 0, rc = 1;
+    double phi = resume ? *phi_io : 1.0;
+    int it = resume ? *iters : 0, rc = 1;
     for (; it < X.P.max_iter; ++it) {
         double mu = 0.0;
         for (int k = X.ln; k <= N; k += WAVE) {
@@ -1296,6 +1303,17 @@ __device__ int ipm(Ctx& X, int* iters) {
         mu = wsum(mu) / m;
         if (!isfinite(mu)) { rc = -1; break; }
         if (mu <= X.P.tol && phi <= 1e-12) { rc = 0; break; }
+        if (!resume && mu <= MU_CHECK && phi <= MU_CHECK) {
+            double tie = 0.0;
+            for (int k = X.ln; k <= N; k += WAVE) {
+                const int nr = stage_nrows(k, N, X.fin);
+                for (int j = 0; j < nr; ++j) {
+                    const double sv = L[Y.oS + NR * k + j], lv = L[Y.oLAM + NR * k + j];
+                    if (!(sv > CHECK_SEP * lv || lv > CHECK_SEP * sv)) tie = 1.0;
+                }
+            }
+            if (wmax(tie) == 0.0) { rc = 2; break; }
+        }
         if (X.dbg & 1) (void)factor_reg(X, 0);
         if (!factor_reg(X, 0)) { rc = -1; break; }
         const double rE[2] = {X.e[0] - L[Y.oZ + ZS * N + 0], X.e[1] - L[Y.oZ + ZS * N + 4]};
@@ -1399,6 +1417,7 @@ __device__ int ipm(Ctx& X, int* iters) {
     }
     sync();
     *iters = it;
+    *phi_io = phi;
     return rc;
 }
 
@@ -1453,7 +1472,27 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
             }
         }
     }
-    const int rc = ipm(X, iters);
+    double phi = 1.0;
+    int rc = ipm(X, iters, false, &phi);
+    if (rc == 2) {
+        // checkpoint (oracle qp_solve): polish from the loose interior point's classification; the interior
+        // point resumes where it stopped if that does not certify
+        for (int k = X.ln; k <= N; k += WAVE) {
+            L[Y.oTACT + k] = ipm_mask(X, k);
+#pragma unroll
+            for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
+        }
+        sync();
+        for (int round = 0; round < CHECK_ROUNDS; ++round) {
+            const int bad = eqp(X, scale);
+            if (bad < 0) break;
+            if (bad == 0) {
+                accept_polish(X, true);
+                return 0;
+            }
+        }
+        rc = ipm(X, iters, true, &phi);
+    }
     if (rc < 0) return -1;
     const double nu_ipm[2] = {X.nu[0], X.nu[1]};
     for (int k = X.ln; k <= N; k += WAVE) {
