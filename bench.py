@@ -508,7 +508,10 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
     wb = W.plan_batch_ref(r, hi - lo, seed=7, offset=lo)
     Bl = hi - lo
     Nv = wb["N"]
-    pl = mpcplan.Planner(r, mpcplan.default_params(N=int(Nv.max())))
+    # the rank's own device: the context's route and every launch live on cuda:LOCAL_RANK
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=int(Nv.max())), device=dev.index)
+    if pl.device != dev.index:
+        raise RuntimeError(f"planner context on device {pl.device}, the rank's device is {dev.index}")
     t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
     x0, st, fin, Nd = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32), t(Nv, torch.int32)
     groups = []

@@ -11,7 +11,8 @@
  *
  * Here B independent chunks (any mix of routes' positions, intermediate or final) are solved in one call:
  * a Gauss-Newton SQP on the same NLP, each QP by a Mehrotra primal-dual interior point on the stage-wise
- * Riccati recursion, FP64, one chunk per GPU lane ("Offline planner").
+ * Riccati recursion, FP64.  One 64-lane wavefront (one workgroup) per chunk, the chunk's whole working set
+ * in that workgroup's LDS; stage-parallel work runs lane k on stage k ("Offline planner").
  *
  * Reference quirks restated:
  *   - the defect rule.  The committed source computes x_pred = x_k - dt/6 (f_k + 4 f_mid + f_{k+1})
@@ -91,11 +92,13 @@ int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const 
                       const int* is_final, double* X, double* U, double* S, int* status, int* iters,
                       int* sqp);
 
-/* Same with device pointers, asynchronous on `stream` (hipStream_t; NULL = the null stream).  Nmax must
- * bound every N[b] (N NULL: params N); a chunk whose N[b] lies outside [1, Nmax] is not solved (zero plan,
- * status PLAN_NUMERICAL).  The kernel needs no scratch memory: each chunk's working set lives in LDS
- * (about 2.4 KB per stage, sized for Nmax; Nmax is limited by the device's LDS per workgroup, 64 at 160 KB),
- * so the call allocates nothing and can be captured into a graph. */
+/* Same with device pointers, asynchronous on `stream` (hipStream_t; NULL = the null stream).  Nmax is the
+ * row stride of X, U and S in every case and must bound every N[b]; with N NULL every chunk has the params'
+ * horizon N and Nmax < params N is PLAN_E_ARG (rows past a chunk's horizon are written as zero).  A chunk
+ * whose N[b] lies outside [1, Nmax] is not solved (zero plan, status PLAN_NUMERICAL).  The kernel needs no
+ * scratch memory: each chunk's working set lives in LDS (about 2.1 KB per stage, sized for Nmax; Nmax is
+ * limited by the device's LDS per workgroup, 64 at 160 KB), so the call allocates nothing and can be
+ * captured into a graph. */
 int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const double* x0,
                              const double* s_target, const int* is_final, double* X, double* U, double* S,
                              int* status, int* iters, int* sqp, void* stream);

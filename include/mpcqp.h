@@ -27,7 +27,9 @@
 extern "C" {
 #endif
 
-#define MPCQP_VERSION 1
+/* 2: status[] / hist_status[] may carry the MPC_SQP_UNCONVERGED flag (16) OR-ed onto the code; mask with
+ *    MPC_STATUS_MASK before comparing with MPC_OK .. MPC_NUMERICAL (version 1 returned 0-3 only). */
+#define MPCQP_VERSION 2
 #define MPC_MAX_N 63          /* horizon limit (one lane per stage k=0..N in the kernel)   */
 #define MPC_MAX_OBS 64        /* obstacle slab limit per instance                            */
 

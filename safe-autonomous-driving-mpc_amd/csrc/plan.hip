@@ -9,15 +9,14 @@
 //   active-set crossover from the previous QP's active rows, else a Mehrotra interior point on the
 //   stage-wise Riccati recursion followed by the same equality-constrained solve ("polish").
 //
-// Mapping: one wavefront (one 64-lane workgroup) = one chunk, its whole working set in LDS (about 48 KB at
-// N = 20: three chunks per CU).  Everything that is independent per stage runs stage-parallel, lane k on
-// stage k: the linearisation (Hermite-Simpson Jacobians, the exact-Hessian fold), the barrier-weighted stage
-// Hessians, the interior point's row residuals, directions, ratio tests and updates, the merit evaluations
-// of the line search (defects of every interval), the multiplier recovery.  The Riccati factorisation and
-// its backward / forward recursions are sequential in the stage and run on lane 0 out of LDS.  Reductions
-// (complementarity, step lengths, norms) are wave shuffles.  A lane-per-chunk version with the state in
-// global scratch (round 4, first cut) was latency-bound at one wave per SIMD and ran ~300 chunks/s at N = 20;
-// a wave also waited for its slowest chunk.  Here every chunk retires on its own.
+// Mapping: one wavefront (one 64-lane workgroup) = one chunk, its whole working set in LDS (265 doubles per
+// stage, about 37 KB at N = 16: four chunks per CU).  Everything that is independent per stage runs
+// stage-parallel, lane k on stage k: the linearisation (Hermite-Simpson Jacobians, the exact-Hessian fold),
+// the barrier-weighted stage Hessians, the interior point's row residuals, directions, ratio tests and
+// updates, the merit evaluations of the line search (defects of every interval), the multiplier recovery.
+// The Riccati factorisation and its backward / forward recursions are sequential in the stage and run
+// lane-distributed inside the wave (plan_kernel.h: factor_par, solve_core).  Reductions (complementarity,
+// step lengths, norms) are wave shuffles.  Every chunk's wave retires on its own.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -170,8 +169,9 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
     if (B < 0) return fail(PLAN_E_ARG, "B must be >= 0");
     if (B == 0) return PLAN_SUCCESS;
     if (!x0 || !s_target) return fail(PLAN_E_ARG, "x0 and s_target are required");
-    if (!N) Nmax = c->p.N;
+    // Nmax is always the caller's row stride; without per-chunk N every chunk has the params' horizon
     if (Nmax < 1 || Nmax > PLAN_MAX_N) return fail(PLAN_E_ARG, "Nmax out of range [1, PLAN_MAX_N]");
+    if (!N && Nmax < c->p.N) return fail(PLAN_E_ARG, "Nmax must be >= params N when N is NULL (Nmax is the row stride)");
     const size_t lds = lds_bytes(Nmax);
     if (lds > c->lds_max) return fail(PLAN_E_ARG, "Nmax too large for the device's LDS");
     if (hipSetDevice(c->device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");

@@ -98,14 +98,18 @@ def _pi(a):
 class Planner:
     """One libmpcplan context: a device-resident route (routes.Route) and the planner parameters."""
 
+    created = 0          # contexts created in this process (plan_create calls that succeeded)
+
     def __init__(self, route, params=None, device=0):
         self.route = route
+        self.device = int(device)
         self.params = params if params is not None else default_params()
         arr = [np.ascontiguousarray(a, np.float64) for a in (route.s, route.cx, route.cy, route.vmax)]
         h = C.c_void_p()
         _check(lib().plan_create(_p(arr[0]), len(arr[0]), _p(arr[1]), _p(arr[2]), _p(arr[3]), C.byref(self.params),
                                  int(device), C.byref(h)), "plan_create")
         self.h = h
+        Planner.created += 1
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:

@@ -18,7 +18,11 @@ and `synthetic` (a documented generator: curvature profile + speed-limit bands).
 import math
 
 import numpy as np
-from scipy.interpolate import CubicSpline, interp1d
+from scipy.interpolate import CubicSpline, PPoly, interp1d
+
+
+def _is_interp1d(f, kind):
+    return isinstance(f, interp1d) and getattr(f, "_kind", None) == kind
 
 
 def add_extra_points(p1, p2, threshold=5.0):
@@ -46,24 +50,68 @@ class Route:
         pts = np.asarray(detailed_points, np.float64)
         if pts.ndim != 2 or pts.shape[1] != 2 or pts.shape[0] < 3:
             raise ValueError("need at least 3 detailed way-points (M, 2)")
+        t = np.arange(len(pts))
+        spline = (CubicSpline(t, pts[:, 0]), CubicSpline(t, pts[:, 1]))              # create_spline
+        dist = np.sqrt(np.diff(pts[:, 0]) ** 2 + np.diff(pts[:, 1]) ** 2)              # :412
+        s = np.concatenate([[0], np.cumsum(dist)])                                     # :413
+        self._set(name, pts, spline, s, v_max_points)
+
+    def _set(self, name, pts, spline, s, v_max_points, s_to_t=None, vint=None):
         self.name = name
         self.points = pts
-        t = np.arange(len(pts))
-        self.spline = (CubicSpline(t, pts[:, 0]), CubicSpline(t, pts[:, 1]))        # create_spline
-        dist = np.sqrt(np.diff(pts[:, 0]) ** 2 + np.diff(pts[:, 1]) ** 2)              # :412
-        self.s = np.concatenate([[0], np.cumsum(dist)])                                # :413
-        if not (np.diff(self.s) > 0).all():
-            raise ValueError("consecutive way-points must be distinct")
+        self.spline = spline
+        self.s = np.ascontiguousarray(s, np.float64)
+        if self.s.ndim != 1 or self.s.size < 3 or not (np.diff(self.s) > 0).all():
+            raise ValueError("consecutive way-points must be distinct (s strictly increasing, at least 3 points)")
         self.s_total = float(self.s[-1])                                               # :414
-        self.cx = np.ascontiguousarray(self.spline[0].c.T)                            # [M-1][4], cubic first
-        self.cy = np.ascontiguousarray(self.spline[1].c.T)
+        self.cx = np.ascontiguousarray(spline[0].c.T, np.float64)                     # [M-1][4], cubic first
+        self.cy = np.ascontiguousarray(spline[1].c.T, np.float64)
+        if self.cx.shape != (self.s.size - 1, 4) or self.cy.shape != self.cx.shape:
+            raise ValueError("the spline must have one cubic piece per way-point interval")
         self.vmax = np.ascontiguousarray(v_max_points, np.float64)
-        if self.vmax.shape != (len(pts),):
+        if self.vmax.shape != self.s.shape:
             raise ValueError("one speed limit per detailed way-point")
         # the reference's own route functions (trajectory_planning.py:440-473), for checks and the drop-in
-        self._s_to_t = interp1d(self.s, np.linspace(0.0, len(pts) - 1, len(pts)), kind="linear",
-                                fill_value="extrapolate")
-        self._vint = interp1d(self.s, self.vmax, kind="previous", fill_value="extrapolate")
+        M = self.s.size
+        self._s_to_t = s_to_t if s_to_t is not None else interp1d(self.s, np.linspace(0.0, M - 1, M), kind="linear",
+                                                                   fill_value="extrapolate")
+        self._vint = vint if vint is not None else interp1d(self.s, self.vmax, kind="previous",
+                                                            fill_value="extrapolate")
+
+    @classmethod
+    def from_reference_functions(cls, s_to_t, spline, v_max_interpolator, name="route"):
+        """The route behind the closures optimize_full_trajectory builds (trajectory_planning.py:440-473): s_to_t
+        (interp1d linear, s_values -> t_values), the CubicSpline pair of the reference path, and
+        v_max_interpolator (interp1d 'previous' over the speed-limit array).  The arrays are taken from those
+        objects as they are (no refit), so the device route is the reference's own spline and limits."""
+        if not (_is_interp1d(s_to_t, "linear") and _is_interp1d(v_max_interpolator, "previous")):
+            raise TypeError("s_to_t must be interp1d(kind='linear') and v_max_interpolator interp1d(kind='previous')")
+        s = np.asarray(s_to_t.x, np.float64)
+        M = s.size
+        if not np.array_equal(np.asarray(s_to_t.y, np.float64), np.linspace(0.0, M - 1, M)):
+            raise ValueError("s_to_t must map s_values to t = 0 .. M-1 (trajectory_planning.py:440-442)")
+        if not np.array_equal(np.asarray(v_max_interpolator.x, np.float64), s):
+            raise ValueError("v_max_interpolator and s_to_t are over different s_values")
+        if len(spline) != 2 or not all(isinstance(p, PPoly) for p in spline):
+            raise TypeError("the reference path spline must be a pair of scipy CubicSpline objects")
+        for p in spline:
+            if p.c.shape != (4, M - 1) or not np.array_equal(np.asarray(p.x, np.float64), np.arange(M, dtype=np.float64)):
+                raise ValueError("the spline pair must be cubic over t = 0 .. M-1 (path_planning.create_spline)")
+        pts = np.column_stack([np.append(spline[0].c[3], spline[0](M - 1.0)), np.append(spline[1].c[3], spline[1](M - 1.0))])
+        r = cls.__new__(cls)
+        r._set(name, pts, tuple(spline), s, np.asarray(v_max_interpolator.y, np.float64), s_to_t, v_max_interpolator)
+        return r
+
+    def content_key(self):
+        """sha256 over the arrays the device holds (s, cx, cy, vmax): equal keys = the same device route."""
+        k = getattr(self, "_key", None)
+        if k is None:
+            import hashlib
+            h = hashlib.sha256()
+            for a in (self.s, self.cx, self.cy, self.vmax):
+                h.update(np.ascontiguousarray(a, np.float64).tobytes())
+            k = self._key = h.hexdigest()
+        return k
 
     @property
     def M(self):

@@ -3,9 +3,11 @@
 `TrajectoryOptimizer` keeps the reference's constructor, attributes, `dynamics`, `unpack` / `pack`, `cost`
 and `optimize(x0, s_target, s_total, k_ref_fun, v_min_fun, v_max_fun, is_final_chunk)` signature
 (trajectory_planning.py:8-391).  The NLP is solved on the GPU (include/mpcplan.h), so the route functions
-must be the ones of a routes.Route (its bound k_ref_fun / v_max_fun, the reference's own :445-473 built from
-the route's spline and speed limits): an arbitrary Python callable cannot be evaluated on the device and
-raises TypeError.  `optimize_full_trajectory(route, max_chunk_size=20)` restates the chunked receding-horizon
+must be ones whose route can be put on the device: the closures optimize_full_trajectory itself builds
+(:442-473; the route is read from their s_to_t, CubicSpline pair and v_max_interpolator) or a routes.Route's
+bound k_ref_fun / v_max_fun.  An arbitrary Python callable raises TypeError.  One device context per distinct
+route is shared by all optimizers (planner_for), so the reference's optimizer-per-chunk loop uploads the
+route once.  `optimize_full_trajectory(route, max_chunk_size=20)` restates the chunked receding-horizon
 loop (:419-559) and ends with reference_trajectory_check (:557).  Route acquisition (path_planning.py,
 GraphHopper over HTTP) is out of scope: routes.py builds the route from local way-points.
 """
@@ -37,7 +39,6 @@ class TrajectoryOptimizer:
         self.a_max = 6.0
         self.device = device
         self.last_status = None
-        self._planners = {}
 
     @staticmethod
     def dynamics(x, u, k_ref):
@@ -80,28 +81,108 @@ class TrajectoryOptimizer:
         return p
 
     def planner(self, route, v_min=0.0):
-        key = (id(route), float(v_min))
-        pl = self._planners.get(key)
-        if pl is None:
-            pl = mpcplan.Planner(route, self.params(v_min), device=self.device)
-            self._planners[key] = pl
-        else:
-            pl.set_params(self.params(v_min))
+        """The route's shared context (planner_for), with this optimizer's parameters."""
+        pl = planner_for(route, self.device)
+        pl.set_params(self.params(v_min))
         return pl
 
     def optimize(self, x0, s_target, s_total, k_ref_fun, v_min_fun, v_max_fun, is_final_chunk):
-        """:351-390 — returns (X [N+1,5], U [N,2], S [N]); the chunk's status is left in self.last_status."""
-        route = getattr(k_ref_fun, "__self__", None)
-        if route is None or getattr(v_max_fun, "__self__", None) is not route or not hasattr(route, "cx"):
-            raise TypeError("the GPU planner evaluates the route on the device: pass k_ref_fun / v_max_fun of a "
-                            "routes.Route (route.k_ref_fun, route.v_max_fun)")
+        """:351-390 — returns (X [N+1,5], U [N,2], S [N]); the chunk's status is left in self.last_status.
+
+        k_ref_fun / v_max_fun are either a routes.Route's bound methods or the closures optimize_full_trajectory
+        builds (:445-473); the route is recovered from them (route_from_functions) and its device context is
+        shared by every optimizer on this device (the reference makes a new optimizer per chunk, :517).
+        v_min_fun must be constant over the chunk (the reference's is 0, :476-477): the device rows take one
+        v_min."""
+        route = route_from_functions(k_ref_fun, v_max_fun)
         if abs(float(s_total) - route.s_total) > 1e-9 * max(1.0, route.s_total):
             raise ValueError("s_total must be the route's total length")
-        v_min = float(v_min_fun(x0[0]))
-        r = self.planner(route, v_min).solve_chunks(np.asarray(x0, np.float64)[None], float(s_target),
+        s0 = float(x0[0])
+        vs = [float(v_min_fun(s)) for s in (s0, 0.5 * (s0 + float(s_target)), float(s_target))]
+        if not (vs[0] == vs[1] == vs[2]):
+            raise TypeError("v_min_fun must be constant over the chunk (the device rows take one v_min; the "
+                            f"reference's is 0): got {vs} at s = x0, midpoint, s_target")
+        r = self.planner(route, vs[0]).solve_chunks(np.asarray(x0, np.float64)[None], float(s_target),
                                                     int(bool(is_final_chunk)), int(self.N))
         self.last_status = int(r["status"][0])
         return r["X"][0], r["U"][0], r["S"][0]
+
+
+# ---- route recovery and the per-route context cache --------------------------------------------------------
+
+_ROUTES = {}          # ids of (s_to_t, spline pair, v_max_interpolator) -> routes.Route holding those objects
+_PLANNERS = {}        # (route content key, device) -> mpcplan.Planner
+MAX_CACHED_ROUTES = 8
+
+
+def _closure(f):
+    code, cells = getattr(f, "__code__", None), getattr(f, "__closure__", None)
+    if code is None or not cells:
+        return {}
+    out = {}
+    for name, c in zip(code.co_freevars, cells):
+        try:
+            out[name] = c.cell_contents
+        except ValueError:          # an empty cell
+            pass
+    return out
+
+
+def route_from_functions(k_ref_fun, v_max_fun):
+    """The routes.Route that k_ref_fun / v_max_fun evaluate.
+
+    - bound methods of one routes.Route: that route;
+    - the closures of optimize_full_trajectory (trajectory_planning.py:442-473): k_ref_fun closes over s_to_t
+      (interp1d linear, s_values -> t) and the reference path's CubicSpline pair, v_max_fun over
+      v_max_interpolator (interp1d 'previous' over v_max_array).  The arrays are read from those objects
+      (s_to_t.x, the splines' .c, v_max_interpolator.y), not refitted.
+    Anything else raises TypeError: an arbitrary callable cannot be evaluated on the device."""
+    import routes
+    from scipy.interpolate import PPoly, interp1d
+    r = getattr(k_ref_fun, "__self__", None)
+    if isinstance(r, routes.Route):
+        if getattr(v_max_fun, "__self__", None) is not r:
+            raise TypeError("k_ref_fun and v_max_fun must be bound to the same routes.Route")
+        return r
+    ck, cv = _closure(k_ref_fun), _closure(v_max_fun)
+    s_to_t = [v for v in ck.values() if isinstance(v, interp1d) and getattr(v, "_kind", None) == "linear"]
+    spl = [v for v in ck.values() if isinstance(v, (tuple, list)) and len(v) == 2
+           and all(isinstance(p, PPoly) for p in v)]
+    vint = [v for v in cv.values() if isinstance(v, interp1d) and getattr(v, "_kind", None) == "previous"]
+    if len(s_to_t) != 1 or len(spl) != 1 or len(vint) != 1:
+        raise TypeError("the GPU planner evaluates the route on the device: pass k_ref_fun / v_max_fun of a "
+                        "routes.Route, or the closures of trajectory_planning.optimize_full_trajectory (k_ref_fun "
+                        "over s_to_t and the CubicSpline pair, v_max_fun over v_max_interpolator)")
+    key = (id(s_to_t[0]), id(spl[0]), id(vint[0]))
+    hit = _ROUTES.get(key)
+    # the objects are the key while they live; a hit must still hold the very same objects
+    if hit is not None and hit._s_to_t is s_to_t[0] and hit._vint is vint[0] and hit.spline[0] is spl[0][0]:
+        return hit
+    r = routes.Route.from_reference_functions(s_to_t[0], spl[0], vint[0], name="reference-closures")
+    if len(_ROUTES) >= MAX_CACHED_ROUTES:
+        _ROUTES.pop(next(iter(_ROUTES)))
+    _ROUTES[key] = r
+    return r
+
+
+def planner_for(route, device=0):
+    """One libmpcplan context per distinct route (content hash of its device arrays) and device, shared by every
+    TrajectoryOptimizer: the reference's per-chunk optimizers (:517) reuse it, so a route is uploaded once.
+    At most MAX_CACHED_ROUTES contexts are kept (the oldest is closed first); release_planners() closes all."""
+    key = (route.content_key(), int(device))
+    pl = _PLANNERS.get(key)
+    if pl is None:
+        if len(_PLANNERS) >= MAX_CACHED_ROUTES:
+            _PLANNERS.pop(next(iter(_PLANNERS))).close()
+        pl = mpcplan.Planner(route, device=device)
+        _PLANNERS[key] = pl
+    return pl
+
+
+def release_planners():
+    """Close every cached planner context."""
+    while _PLANNERS:
+        _PLANNERS.popitem()[1].close()
 
 
 def optimize_full_trajectory(route, max_chunk_size=20, max_chunks=10000, device=0, verbose=False, check=True,
@@ -169,8 +250,6 @@ def optimize_full_trajectory(route, max_chunk_size=20, max_chunks=10000, device=
     optimize_full_trajectory.horizons = horizons
     if check:
         reference_trajectory_check(TrajectoryOptimizer(device=device), X_final, U_final, S_final, s_total)
-    for pl in opt._planners.values():
-        pl.close()
     return X_final, U_final, S_final
 
 

@@ -324,11 +324,12 @@ def test_closed_loop_config1(lib):
     assert "===> Checks passed : True" in buf.getvalue(), buf.getvalue()[-800:]
     g = load_golden("closedloop_golden")
     ref_x = g["c1_traj1_N10_hist_x"]
-    assert abs(len(hx) - len(ref_x)) <= 10
+    # the reference's SLSQP stops at ftol=1e-3 (trajectory_tracking.py:255) and the exact NLP optimum brakes a
+    # step apart from it: steps within +-2, lateral offsets within 0.1 m over the whole run (the bar of the FSM
+    # runs and of the host backend's config-1 loop, tests/test_cpu_backend.py)
+    assert abs(len(hx) - len(ref_x)) <= 2
     m = min(len(hx), len(ref_x))
-    # the reference's SLSQP stops at ftol=1e-3 (trajectory_tracking.py:255), so its closed loop is an
-    # inexact-solver trajectory; the lateral offsets agree to within half a metre over the whole run
-    assert np.abs(hx[:m, 1] - ref_x[:m, 1]).max() < 0.5
+    assert np.abs(hx[:m, 1] - ref_x[:m, 1]).max() < 0.1
 
 
 def test_global_pose_device_vs_golden(lib, solvers):
