@@ -630,6 +630,19 @@ static double max_step(const qpdat* Q, const ipm_state* S, const ipm_dir* D) {
 #define POLISH_REFINE 2
 #define POLISH_ROUNDS 6
 #define XO_ROUNDS 1         /* rounds of the crossover attempt before the interior point */
+#define MU_CHECK 1e-4       /* interior-point checkpoint: a polish is tried once mu is below this ... */
+#define CHECK_SEP 100.0     /* ... and every row's slack and multiplier differ by this factor (no near-tie) */
+#define CHECK_ROUNDS 2      /* polish rounds at the checkpoint (the interior point continues if they fail) */
+/* MPC_CHECKPOINT=0 in the environment switches the checkpoint off (A/B against the round-4 interior point;
+ * the product's libmpcqp reads the same variable) */
+static int check_on(void) {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = getenv("MPC_CHECKPOINT");
+        on = !(e && e[0] == '0');
+    }
+    return on;
+}
 /* Classification left by the last polish_from call of this thread (the accepted one, or the one the last
  * rejected round flipped to): the SQP's next re-linearisation starts its crossover from it (given = 2). */
 static __thread unsigned char last_cls[MAXN + 1][NROW], last_clb[MAXN][NBOX];
@@ -828,6 +841,33 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
     }
 
     double X[MAXN + 1][5];
+    const int start2 = getenv("ORC_START2_N") && N >= atoi(getenv("ORC_START2_N"));
+    double bscale = 0.0, rowc = 0.0;
+    if (start2) {
+        memset(S->du, 0, sizeof(double) * 2 * N);
+        for (int k = 1; k <= N; ++k)
+            for (int j = 0; j < NROW; ++j) {
+                if (!Q->on[j]) continue;
+                const double r0 = -Q->b[k][j];
+                const double xi = (r0 < 0 ? -r0 : 0.0) + 1e-1;
+                const double sv = r0 + xi;
+                const double lam = 1000.0 / sv < 0.5 * rho ? 1000.0 / sv : 0.5 * rho;
+                S->xi[k][j] = xi;
+                S->s[k][j] = sv;
+                S->lam[k][j] = lam;
+                S->nu[k][j] = rho - lam;
+                rowc += S->s[k][j] * S->lam[k][j] + S->xi[k][j] * S->nu[k][j];
+                if (fabs(Q->b[k][j]) > bscale) bscale = fabs(Q->b[k][j]);
+            }
+        const double mrow2 = rowc / (double)(2 * nsoft * N);
+        for (int t = 0; t < N; ++t)
+            for (int j = 0; j < NBOX; ++j) {
+                const double r0 = -Q->bb[t][j];
+                S->sb[t][j] = r0 > 1.0 ? r0 : 1.0;
+                S->lb[t][j] = mrow2 / S->sb[t][j];
+                if (fabs(Q->bb[t][j]) > bscale) bscale = fabs(Q->bb[t][j]);
+            }
+    } else {
     /* Interior-point start (round 3): centred at the unconstrained optimum of QP(ubar) (one Riccati
      * factorisation and solve without rows), or at du = 0 when the soft rows are less violated there.  Each soft row with value r = C x - b there gets slack
      * max(r, 0) + START_SHIFT and elastic slack max(-r, 0) + START_SHIFT, and the multiplier pair on the
@@ -871,7 +911,6 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
             rollout_lin(Q, S->du, X);
         }
     }
-    double bscale = 0.0, rowc = 0.0;
     for (int k = 1; k <= N; ++k)
         for (int j = 0; j < NROW; ++j) {
             if (!Q->on[j]) continue;
@@ -892,12 +931,13 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
             S->lb[t][j] = mrow / S->sb[t][j];
             if (fabs(Q->bb[t][j]) > bscale) bscale = fabs(Q->bb[t][j]);
         }
+    }
     double y[MAXN + 1][5], yc[MAXN + 1][5], ya[MAXN + 1][5], z[MAXN][2], zc[MAXN][2], za[MAXN][2];
     double rp[MAXN + 1][NROW], rx[MAXN + 1][NROW], rpb[MAXN][NBOX];
     double r4[MAXN + 1][NROW], r5[MAXN + 1][NROW], r4b[MAXN][NBOX];
     double gd[2 * MAXN], gc[2 * MAXN], ga[2 * MAXN];
     int status = MPC_MAX_ITER, it;
-    int stall = 0;
+    int stall = 0, checked = 0;
     for (it = 0; it < p->max_iter; ++it) {
         rollout_lin(Q, S->du, X);
         memset(yc, 0, sizeof(yc));
@@ -963,6 +1003,33 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
         if (mu <= p->tol_mu && rpmax <= 10.0 * p->tol * (1.0 + bscale) && rxmax <= p->tol * rho) {
             status = rdmax <= 1e4 * p->tol * (1.0 + sd) ? MPC_OK : MPC_NUMERICAL;
             break;
+        }
+        /* Interior-point checkpoint (once per QP): once mu <= MU_CHECK and every row's
+         * slack and multiplier (s, lambda; xi, nu; box s, lambda) are CHECK_SEP apart, the iterate's
+         * classification is tried by CHECK_ROUNDS polish rounds; a certified point is the QP's exact optimum
+         * (the QP is strictly convex), otherwise the interior point continues from the unchanged iterate. */
+        if (p->polish && !checked && mu <= MU_CHECK && check_on()) {
+            int tie = 0;
+            for (int k = 1; k <= N && !tie; ++k)
+                for (int j = 0; j < NROW; ++j) {
+                    if (!Q->on[j]) continue;
+                    const double s = S->s[k][j], l = S->lam[k][j], x = S->xi[k][j], n = S->nu[k][j];
+                    if (!(s > CHECK_SEP * l || l > CHECK_SEP * s) || !(x > CHECK_SEP * n || n > CHECK_SEP * x)) tie = 1;
+                }
+            for (int t = 0; t < N && !tie; ++t)
+                for (int j = 0; j < NBOX; ++j)
+                    if (!(S->sb[t][j] > CHECK_SEP * S->lb[t][j] || S->lb[t][j] > CHECK_SEP * S->sb[t][j])) tie = 1;
+            if (!tie) {
+                static __thread ipm_state C;
+                int inf = 0;
+                checked = 1;
+                memcpy(&C, S, sizeof(C));
+                if (polish_from(Q, &C, &inf, 0, CHECK_ROUNDS)) {
+                    memcpy(S->du, C.du, sizeof(double) * 2 * N);
+                    *iters = it;
+                    return inf ? MPC_INFEASIBLE : MPC_OK;
+                }
+            }
         }
         factor(Q, S, &F);
         /* predictor */

@@ -36,6 +36,7 @@
 #include "plan_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -59,7 +60,9 @@
 #define CYCLE_REL 1e-6
 #define DELTA0 1e-6           /* first Hessian regularisation when a pivot fails; x10 per retry */
 #define DELTA_MAX 1e4
-#define EXACT_STEP 0.1        /* exact Lagrangian Hessian once the last SQP step is at most this (max norm) */
+#define EXACT_STEP 0.1        /* exact Lagrangian Hessian once the last SQP step is at most this (max norm) ... */
+#define EXACT_AFTER 20        /* ... or from this SQP iteration on (a Gauss-Newton SQP can zigzag with steps of ~0.2
+                                 around an active lateral-acceleration row without ever meeting EXACT_STEP) */
 #define LS_ARMIJO 1e-4        /* line search on the L1 merit f + mu * violation: sufficient decrease */
 #define LS_STEPS 12           /* halvings at most (the last one is taken regardless) */
 #define LS_FULL 1e-3          /* steps at most this long (max norm) are taken whole (local phase) */
@@ -816,7 +819,7 @@ static double row_val(const qp_t* Q, int k, int j, const double z[NZ]) {
     return v;
 }
 
-/* dynamics-feasible start: dx_0 = xi0, dw = 0 */
+/* dynamics-feasible start: dx_0 = xi0, dw = 0 (fused multiply-adds, the kernel's DPP recursion) */
 static void rollout(const qp_t* Q, double z[][NZ]) {
     const int N = Q->N;
     memset(z, 0, sizeof(double) * NZ * (N + 1));
@@ -824,7 +827,7 @@ static void rollout(const qp_t* Q, double z[][NZ]) {
     for (int k = 0; k < N; ++k)
         for (int i = 0; i < 5; ++i) {
             double v = Q->c[k][i];
-            for (int l = 0; l < 5; ++l) v += Q->A[k][5 * i + l] * z[k][l];
+            for (int l = 0; l < 5; ++l) v = fma(Q->A[k][5 * i + l], z[k][l], v);
             z[k + 1][i] = v;
         }
 }
@@ -1013,6 +1016,13 @@ static int ipm(qp_t* Q, const plan_params* p, qpsol_t* X, int* iters, int resume
 
 /* one QP: active-set rounds from the previous classification (when given), else interior point + polish.
  * Returns 0 solved (exact KKT point), 1 interior-point answer without a certified polish, -1 failure. */
+/* diagnostics (PLAN_TRACE=1 in the environment, tools/plan_trace.py): how the last QP was solved -- 'W' warm
+ * active-set rounds (qp_path_n = rounds), 'C' checkpoint polish, 'P' polish after the interior point, 'I' the
+ * interior point's answer uncertified, 'F' failure */
+static __thread char qp_path;
+static __thread int qp_path_n;
+static int plan_trace(void) { return getenv("PLAN_TRACE") != NULL; }
+
 static int qp_solve(qp_t* Q, const plan_params* p, qpsol_t* X, int have_cls, int* iters) {
     static __thread unsigned char act[MAXNP][NR];
     static __thread double z[MAXNP][NZ], lam[MAXNP][NR];
@@ -1036,6 +1046,8 @@ static int qp_solve(qp_t* Q, const plan_params* p, qpsol_t* X, int have_cls, int
                 memcpy(X->act, act, sizeof(act));
                 X->nu[0] = nu[0];
                 X->nu[1] = nu[1];
+                qp_path = 'W';
+                qp_path_n = round + 1;
                 return 0;
             }
         }
@@ -1059,11 +1071,15 @@ static int qp_solve(qp_t* Q, const plan_params* p, qpsol_t* X, int have_cls, int
                 memcpy(X->act, act, sizeof(act));
                 X->nu[0] = nu[0];
                 X->nu[1] = nu[1];
+                qp_path = 'C';
+                qp_path_n = round + 1;
                 return 0;
             }
         }
         rc = ipm(Q, p, X, iters, 1, &phi);
     }
+    qp_path = 'F';
+    qp_path_n = 0;
     if (rc < 0) return -1;
     for (int k = 0; k <= N; ++k)
         for (int j = 0; j < Q->nr[k]; ++j) {
@@ -1119,7 +1135,7 @@ static void multipliers(const qp_t* Q, const qpsol_t* X, mult_t* M) {
             double pn[5];
             for (int i = 0; i < 5; ++i) {
                 double v = g[i];
-                for (int l = 0; l < 5; ++l) v += Q->A[k][5 * l + i] * pi[l];
+                for (int l = 0; l < 5; ++l) v = fma(Q->A[k][5 * l + i], pi[l], v);
                 pn[i] = v;
             }
             memcpy(pi, pn, sizeof(pi));
@@ -1210,7 +1226,8 @@ int orc_plan_chunk(const orc_route* r, const plan_params* p, int N, const double
     int status = PLAN_NOT_CONVERGED, total = 0, nq = 0, have_cls = 0, frozen = 0, since = 0;
     double last = INFINITY;
     for (int it = 0; it < p->sqp_iters; ++it, ++since) {
-        int exact = last <= EXACT_STEP, rc = -1;
+        int exact = last <= EXACT_STEP || it >= EXACT_AFTER, rc = -1;
+        const int tot0 = total;
         for (;;) {
             if (build_qp(r, p, N, x0, s_target, is_final, Xb, Ub, Sb, frozen ? vlim : NULL, exact ? &mult : NULL, &Q)) {
                 rc = -2;
@@ -1272,6 +1289,19 @@ int orc_plan_chunk(const orc_route* r, const plan_params* p, int N, const double
             fin &= isfinite(znew[i]);
         }
         if (!fin) { status = PLAN_NUMERICAL; break; }
+        if (plan_trace()) {
+            int nact = 0, nchg = 0;
+            static __thread unsigned char prev[MAXNP][NR];
+            for (int k = 0; k <= N; ++k)
+                for (int j = 0; j < Q.nr[k]; ++j) {
+                    nact += sol.act[k][j];
+                    nchg += it > 0 && sol.act[k][j] != prev[k][j];
+                    prev[k][j] = sol.act[k][j];
+                }
+            fprintf(stderr, "sqp %3d %s qp %c%d ipm %4d act %3d chg %3d |dz| %.3e alpha %.4g step %.3e back2 %.3e "
+                    "frozen %d delta %.1e\n", it, exact ? "exact" : "gn   ", qp_path, qp_path_n, total - tot0, nact, nchg, full, alpha,
+                    step, back2, frozen, Q.delta);
+        }
         memcpy(z2, zb, sizeof(double) * nz);
         memcpy(zb, znew, sizeof(double) * nz);
         last = step;

@@ -38,6 +38,17 @@ constexpr int kRows = 9;          // soft rows per stage: lane +-d, +-(d + L/2 o
 constexpr int kBox = 4;           // box rows per control: +u1, -u1, +u2, -u2
 constexpr double kTau = 0.995;    // the device constants (mpcqp.hip: TAU, START_SHIFT, POLISH_*, SQP_*)
 constexpr double kStartShift = 3.0;
+constexpr double kMuCheck = 1e-4;     // interior-point checkpoint (mpcqp.hip: MU_CHECK, CHECK_SEP, CHECK_ROUNDS)
+constexpr double kCheckSep = 100.0;
+constexpr int kCheckRounds = 2;
+// MPC_CHECKPOINT=0 in the environment switches the checkpoint off (A/B; the device kernels read the same flag)
+inline bool checkpoint_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("MPC_CHECKPOINT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 constexpr double kDelta = 1e-11;
 constexpr int kRefine = 2;
 constexpr int kPolishRounds = 6;
@@ -217,7 +228,7 @@ private:
     const Ref& R_;
     const mpc_params& p_;
     StageQp q_;
-    IpState S_, Z_, T_;
+    IpState S_, Z_, T_, C_;
     Factors F_;
     Direction D_, Da_;
     unsigned char cls_[kMaxN + 1][kRows], clb_[kMaxN][kBox];      // 0 inactive, 1 active, 2 violated
@@ -755,6 +766,7 @@ private:
         double rp[kMaxN + 1][kRows], rx[kMaxN + 1][kRows], rpb[kMaxN][kBox];
         double r4[kMaxN + 1][kRows], r5[kMaxN + 1][kRows], r4b[kMaxN][kBox];
         int status = MPC_MAX_ITER, it = 0, stall = 0;
+        bool checked = false;
         for (it = 0; it < p_.max_iter; ++it) {
             rollout(S_.du, X);
             double rpmax = 0.0, rxmax = 0.0, comp = 0.0;
@@ -805,6 +817,31 @@ private:
                 }
                 status = rdmax <= 1e4 * p_.tol * (1.0 + sd) ? MPC_OK : MPC_NUMERICAL;
                 break;
+            }
+            // checkpoint (once per QP): no near-tie between any row's slack and multiplier at mu <= kMuCheck ->
+            // kCheckRounds polish rounds from the iterate's classification; certified = the exact optimum, else
+            // the interior point continues from the unchanged iterate
+            if (p_.polish && !checked && mu <= kMuCheck && checkpoint_on()) {
+                bool tie = false;
+                for (int k = 1; k <= N && !tie; ++k)
+                    for (int j = 0; j < kRows; ++j) {
+                        if (!Q.on[j]) continue;
+                        const double s = S_.s[k][j], l = S_.l[k][j], x = S_.xi[k][j], n = S_.nu[k][j];
+                        if (!(s > kCheckSep * l || l > kCheckSep * s) || !(x > kCheckSep * n || n > kCheckSep * x)) tie = true;
+                    }
+                for (int t = 0; t < N && !tie; ++t)
+                    for (int j = 0; j < kBox; ++j)
+                        if (!(S_.sb[t][j] > kCheckSep * S_.lb[t][j] || S_.lb[t][j] > kCheckSep * S_.sb[t][j])) tie = true;
+                if (!tie) {
+                    checked = true;
+                    std::memcpy(&C_, &S_, sizeof(C_));
+                    bool inf = false;
+                    if (active_set(C_, 0, kCheckRounds, inf)) {
+                        std::memcpy(S_.du, C_.du, sizeof(double) * 2 * N);
+                        iters = it;
+                        return inf ? MPC_INFEASIBLE : MPC_OK;
+                    }
+                }
             }
             factor();
             // predictor (affine scaling)

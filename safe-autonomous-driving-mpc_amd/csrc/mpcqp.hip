@@ -67,6 +67,7 @@ struct KParams {
     double w_d, w_o, w_v, w_u1, w_u2;
     double osd, tgap, L, sl, brake_distance, brake_accel;
     double tol, tol_mu, rho, sqp_tol;
+    double mu_check;   // interior-point checkpoint threshold (MU_CHECK; -1 = off, MPC_CHECKPOINT=0)
     int dbg;           // diagnostics only (MPC_DBG, default 0): 1 = the crossover kernel defers without the
                        // work-list atomic (timing probe; the interior-point launch then sees an empty list)
 };
@@ -1021,6 +1022,12 @@ __device__ unsigned long long g_prof[16];
 #define SQP_CYCLE_REL 1e-6
 #define SQP_INF_STREAK 5
 #define START_SHIFT 3.0     // interior-point start: slack and elastic slack beyond the row value (oracle pdip)
+// interior-point checkpoint (oracle pdip): once mu <= MU_CHECK and every row's slack and
+// multiplier are CHECK_SEP apart, CHECK_ROUNDS polish rounds try the iterate's classification; a certified point
+// is the QP's exact optimum, otherwise the interior point continues from the unchanged iterate (once per QP)
+#define MU_CHECK 1e-4
+#define CHECK_SEP 100.0
+#define CHECK_ROUNDS 2
 
 // ------------------------------------------------------------------------------------------
 // the solver kernel.  A 64-lane wavefront carries G = 64 / GL MPC instances, one per aligned group
@@ -1288,6 +1295,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
         for (int phase = phase_lo; phase < phase_hi; ++phase) {
         bool accepted = false;
         double bad = 0.0;
+        // checkpoint: chk = the interior point stopped there (segment end), checked = it was tried this QP
+        bool chk = false, checked = false;
         if (phase == 1) {
             // Start centred at the unconstrained optimum of QP(ubar) (oracle pdip): one
             // factorisation and solve without rows gives du and the state x4 of stage k there (or du = 0, see
@@ -1356,8 +1365,11 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 lb[j] = mrow * frcp(sb[j]);
             }
             wave_sync();
+        }
+        for (;;) {      // segments: interior point (to convergence or the checkpoint), polish; resume if needed
+        if (phase == 1) {
         PROF(0)
-        for (int iter = 0; iter < Pr.max_iter; ++iter) {
+        for (int iter = it; iter < Pr.max_iter; ++iter) {
             PROF(1)
             // the row bounds are loop-invariant; keeping them opaque stops the compiler from hoisting
             // everything derived from them out of this loop (it would stay live in registers and spill)
@@ -1441,6 +1453,22 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 st_here = rdmax <= 1e4 * Pr.tol * (1.0 + sd) ? MPC_OK : MPC_NUMERICAL;
                 it = iter;
                 break;
+            }
+            if (Pr.polish && !checked && mu <= Pr.mu_check) {
+                double tie = 0.0;
+#pragma unroll
+                for (int j = 0; j < NR; ++j)
+                    if (rowon[j] && (!(rs[j] > CHECK_SEP * rl[j] || rl[j] > CHECK_SEP * rs[j]) ||
+                                     !(rxi[j] > CHECK_SEP * rnu[j] || rnu[j] > CHECK_SEP * rxi[j])))
+                        tie = 1.0;
+#pragma unroll
+                for (int j = 0; j < NBOX; ++j)
+                    if (!(sb[j] > CHECK_SEP * lb[j] || lb[j] > CHECK_SEP * sb[j])) tie = 1.0;
+                if (Q.max(live ? tie : 0.0) == 0.0) {
+                    chk = true;
+                    it = iter;
+                    break;
+                }
             }
             // -- barrier weights, augmented stage Hessians ---------------------------------------
             double il[NR], inu[NR], wv[NR], ilb[NBOX], wb[NBOX];
@@ -1657,6 +1685,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             it = iter + 1;
             if (stall >= 5 || breakdown) { st_here = MPC_NUMERICAL; break; }
         }
+        if (!chk) {
         total_it += it;
         // NaN guard and the infeasibility flag
         if (live) bad = (du0 == du0 && du1 == du1) ? 0.0 : 1.0;
@@ -1671,6 +1700,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             for (int j = 0; j < NR; ++j)
                 if (ron[j] && rxi[j] > 1e-6 * (1.0 + fabs(bk[j]))) inf = 1.0;
             if (Q.max(inf) > 0.0) st_here = MPC_INFEASIBLE;
+        }
         }
         wave_sync();
         }   // phase 1: interior point
@@ -1701,7 +1731,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             // the interior-point iterate (du, x4) is the start of every round and the fallback
             double pu0 = du0, pu1 = du1;
             double nviol_acc = 0.0;
-            const int rounds = phase == 0 ? XO_ROUNDS : POLISH_ROUNDS;
+            const int rounds = phase == 0 ? XO_ROUNDS : (chk ? CHECK_ROUNDS : POLISH_ROUNDS);
             for (int round = 0; round < rounds; ++round) {
                 double tl[NR], tlb[NBOX];
 #pragma unroll
@@ -1868,6 +1898,16 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             }
             wave_sync();
         }
+        if (chk) {
+            if (!accepted) {          // not certified: the interior point continues from the unchanged iterate
+                chk = false;
+                checked = true;
+                continue;
+            }
+            total_it += it;
+        }
+        break;
+        }   // segments
         if (phase == 0) xo_ok = accepted;
         if (accepted || phase == 1) break;
         }   // phases
@@ -2307,6 +2347,7 @@ static KParams kparams(const mpc_params* p) {
     k.sqp_tol = p->sqp_tol;
     const char* dbg = std::getenv("MPC_DBG");
     k.dbg = dbg ? std::atoi(dbg) : 0;
+    k.mu_check = mpcqp_cpu::checkpoint_on() ? MU_CHECK : -1.0;
     return k;
 }
 

@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -53,7 +54,28 @@ struct plan_ctx {
     // host-entry staging
     void* io;
     size_t io_bytes;
+    // longest-first dispatch (plan_order_*_kernel): one buffer per stream the context launches on (2 *
+    // ORDER_BUCKETS counters, then bucket[cap], order[cap]), so calls on different streams never share one;
+    // allocated on a stream's first eager call (a call being captured into a graph without a buffer for its
+    // stream, or a batch above cap_order, runs in index order: same results)
+    std::vector<std::pair<void*, int*>> order_bufs;
+    std::mutex order_mu;
+    int cap_order;
+    bool order_on;
 };
+
+// the stream's order buffer, or nullptr (capturing without one, or allocation failure: index order)
+static int* order_buffer(plan_ctx* c, void* stream) {
+    std::lock_guard<std::mutex> g(c->order_mu);
+    for (auto& e : c->order_bufs)
+        if (e.first == stream) return e.second;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* buf = nullptr;
+    if (hipMalloc(&buf, sizeof(int) * (2 * (size_t)ORDER_BUCKETS + 2 * (size_t)c->cap_order)) != hipSuccess) return nullptr;
+    c->order_bufs.emplace_back(stream, buf);
+    return buf;
+}
 
 static int check_params(const plan_params* p) {
     if (!p) return fail(PLAN_E_ARG, "params is NULL");
@@ -142,6 +164,9 @@ int plan_create(const double* s, int M, const double* cx, const double* cy, cons
     c->R.ginv = ginv;
     c->R.M = M;
     c->R.s_total = s[M - 1];
+    c->cap_order = 1 << 17;
+    const char* oe = std::getenv("PLAN_ORDER");        // PLAN_ORDER=0: index order (A/B)
+    c->order_on = !(oe && oe[0] == '0');
     *out = c;
     return PLAN_SUCCESS;
 }
@@ -159,6 +184,7 @@ void plan_destroy(plan_ctx* c) {
     (void)hipDeviceSynchronize();
     if (c->d_route) (void)hipFree(c->d_route);
     if (c->io) (void)hipFree(c->io);
+    for (auto& e : c->order_bufs) (void)hipFree(e.second);
     delete c;
 }
 
@@ -192,6 +218,23 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
     a.N = N;
     a.x0 = x0;
     a.st = s_target;
+    a.order = nullptr;
+    int* obuf = (c->order_on && B >= 2 * WAVE && B <= c->cap_order) ? order_buffer(c, stream) : nullptr;
+    if (obuf) {
+        int* cnt = obuf;
+        int* bucket = cnt + 2 * ORDER_BUCKETS;
+        int* order = bucket + c->cap_order;
+        const int nb = (B + 255) / 256;
+        if (hipMemsetAsync(cnt, 0, sizeof(int) * 2 * ORDER_BUCKETS, (hipStream_t)stream) != hipSuccess)
+            return fail(PLAN_E_LAUNCH, "order reset failed");
+        hipLaunchKernelGGL(plan_order_count_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, c->R, c->p, B, x0,
+                           s_target, bucket, cnt);
+        hipLaunchKernelGGL(plan_order_scatter_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, B, bucket, cnt,
+                           cnt + ORDER_BUCKETS, order);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess)
+            return fail(PLAN_E_LAUNCH, std::string("order kernels failed: ") + hipGetErrorString(e));
+        a.order = order;
+    }
     a.fin = is_final;
     a.X = X;
     a.U = U;

@@ -42,6 +42,7 @@ constexpr double CYCLE_REL = 1e-6;
 constexpr double DELTA0 = 1e-6;
 constexpr double DELTA_MAX = 1e4;
 constexpr double EXACT_STEP = 0.1;
+constexpr int EXACT_AFTER = 20;      // exact Hessian from this SQP iteration on as well (oracle EXACT_AFTER)
 constexpr double LS_ARMIJO = 1e-4;
 constexpr int LS_STEPS = 12;
 constexpr double LS_FULL = 1e-3;
@@ -832,234 +833,316 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
     }
 }
 
-// v of lane src in every lane (v_readlane into scalar registers: no LDS round trip)
-#ifndef PLAN_HOST_EMU
-__device__ inline double bcast(double v, int src) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
-    return __hiloint2double(hi, lo);
-}
-#endif
+// ------------------------------------------------------------------------------------------------------
+// Riccati recursions on lanes 0..7 with DPP broadcasts (round 5; round 4 read P and [A B] element by element
+// from LDS in every lane of an entry-parallel factorisation and broadcast the solves' vectors by readlane).
+// Lane j holds column j of the stage matrices: of P (j < 5; P is symmetric, so its columns are its rows), of
+// P [A B] and of M = HT + [A B]' P [A B] (j < 7: the five state columns, then u1, u2); in the solves and
+// rollouts, component i of the co-state / state.  Every cross-lane term is one v_fmac_f64_dpp with
+// row_newbcast:l -- lane l's register broadcast within the 16-lane row, fused into the FMA, one issue slot --
+// so nothing of a recursion goes through LDS but the stage data it consumes.  Each sum accumulates its terms
+// in the order oracle/plan_oracle.c uses (factor(), solve_core(), rollout(), multipliers()), one rounding per
+// term, so the two agree bit for bit.  The symmetrisation P <- (Pn + Pn') / 2 pairs lane j's column with the
+// row lane j needs from the other lanes by a per-lane selector (0.5 on the lane's own index, 0 elsewhere):
+// fma(0.5, Pn(j, i), 0.5 Pn(i, j)) = 0.5 (Pn(i, j) + Pn(j, i)) exactly (scaling by 2 commutes with rounding).
+// On the device the recursions run under an exec mask of lanes 0..7 (REC_LANES); the host emulation
+// (tools/plan_emu.cpp) runs them on every lane, since its broadcasts meet at a barrier of all 64 threads.
+// ------------------------------------------------------------------------------------------------------
 
-// LQ solve over the wave with zero initial state and homogeneous dynamics: stage linear terms at ogl ->
-// odz (lane 0 stores; the caller syncs before reading odz).  Per stage the 3-vectors (control rhs, Cholesky
-// solve, feedback) are computed by every lane alike, and the 5-vectors of the recursions (co-state p
-// backwards, state x forwards) one entry per lane on lanes 0..4 and broadcast by readlane.  Every entry
-// is formed by the same operations in the same order as on one lane, so the result is the same.
-// stage records of the two sweeps, loaded one stage ahead (software pipelining: the LDS latency of stage
-// k - 1's data overlaps stage k's arithmetic)
-struct BwdRec {
-    double Lc[6], B0[5], B1[5], gw[3], gx, Acol[5], Kcol[3];
-};
-struct FwdRec {
-    double K[15], Arow[5], Brow[2];
-};
-__device__ inline void load_bwd(const Ctx& X, int ogl, int k, int me, BwdRec& R) {
-    ldsd* L = X.L;
-    const Layout& Y = X.Y;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) R.Lc[i] = L[Y.oL + 6 * k + i];
-#pragma unroll
-    for (int l = 0; l < 5; ++l) {
-        R.B0[l] = L[Y.oB + 10 * k + 2 * l];
-        R.B1[l] = L[Y.oB + 10 * k + 2 * l + 1];
-        R.Acol[l] = L[Y.oA + 25 * k + 5 * l + me];
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        R.gw[i] = L[ogl + ZS * k + 5 + i];
-        R.Kcol[i] = L[Y.oK + 15 * k + 5 * i + me];
-    }
-    R.gx = L[ogl + ZS * k + me];
-}
-__device__ inline void load_fwd(const Ctx& X, int k, int me, FwdRec& R) {
-    ldsd* L = X.L;
-    const Layout& Y = X.Y;
-#pragma unroll
-    for (int i = 0; i < 15; ++i) R.K[i] = L[Y.oK + 15 * k + i];
-#pragma unroll
-    for (int l = 0; l < 5; ++l) R.Arow[l] = L[Y.oA + 25 * k + 5 * me + l];
-    R.Brow[0] = L[Y.oB + 10 * k + 2 * me];
-    R.Brow[1] = L[Y.oB + 10 * k + 2 * me + 1];
-}
 #ifndef PLAN_HOST_EMU
-#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#define REC_LANES(ln) ((ln) < 8)
+// d += s@L * c: s broadcast from lane L of the 16-lane row (DPP row_newbcast), fused into the FMA.  Every asm
+// block starts with s_nop 1, the two wait states a DPP read needs after a VALU write of its source.
+#define PF(d, s, c, L) "v_fmac_f64_dpp " d ", " s ", " c " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
 #else
-#define SCHED_FENCE()
+#define REC_LANES(ln) true
 #endif
 
+// acc += sum_l src@l * c[l] (l = 0..4, in that order): one lane's dot product with a vector held one
+// component per lane (the solves' A' p, A x, K x rows)
+__device__ inline void dot5_lanes(double& acc, double src, const double c[5]) {
+#ifndef PLAN_HOST_EMU
+    asm("s_nop 1\n\t" PF("%0", "%1", "%2", 0) PF("%0", "%1", "%3", 1) PF("%0", "%1", "%4", 2) PF("%0", "%1", "%5", 3)
+        PF("%0", "%1", "%6", 4)
+        : "+&v"(acc) : "v"(src), "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]));
+#else
+    for (int l = 0; l < 5; ++l) acc = fma(dpp_row_bcast(src, l), c[l], acc);
+#endif
+}
+
+// column j of P [A B]: q[i] = sum_l P(i, l) AB(l, j), P(i, l) = register i of lane l (oracle factor(): PA, PB)
+__device__ inline void fac_pab(double q[5], const double Pc[5], const double abc[5]) {
+#ifndef PLAN_HOST_EMU
+#define PAB_L(L, A) PF("%0", "%5", A, L) PF("%1", "%6", A, L) PF("%2", "%7", A, L) PF("%3", "%8", A, L) PF("%4", "%9", A, L)
+    asm("s_nop 1\n\t" PAB_L(0, "%10") PAB_L(1, "%11") PAB_L(2, "%12") PAB_L(3, "%13") PAB_L(4, "%14")
+        : "+&v"(q[0]), "+&v"(q[1]), "+&v"(q[2]), "+&v"(q[3]), "+&v"(q[4])
+        : "v"(Pc[0]), "v"(Pc[1]), "v"(Pc[2]), "v"(Pc[3]), "v"(Pc[4]), "v"(abc[0]), "v"(abc[1]), "v"(abc[2]), "v"(abc[3]),
+          "v"(abc[4]));
+#undef PAB_L
+#else
+    for (int l = 0; l < 5; ++l)
+        for (int i = 0; i < 5; ++i) q[i] = fma(dpp_row_bcast(Pc[i], l), abc[l], q[i]);
+#endif
+}
+
+// column j of M: m[u] += sum_l AB(l, u) (P [A B])(l, j), AB(l, u) = register l of lane u (oracle factor():
+// the A'PA part of Pn, Hwx, Hww)
+__device__ inline void fac_m(double m[8], const double abc[5], const double q[5]) {
+#ifndef PLAN_HOST_EMU
+#define M_L(S, C) PF("%0", S, C, 0) PF("%1", S, C, 1) PF("%2", S, C, 2) PF("%3", S, C, 3) PF("%4", S, C, 4) \
+    PF("%5", S, C, 5) PF("%6", S, C, 6)
+    asm("s_nop 1\n\t" M_L("%7", "%12") M_L("%8", "%13") M_L("%9", "%14") M_L("%10", "%15") M_L("%11", "%16")
+        : "+&v"(m[0]), "+&v"(m[1]), "+&v"(m[2]), "+&v"(m[3]), "+&v"(m[4]), "+&v"(m[5]), "+&v"(m[6])
+        : "v"(abc[0]), "v"(abc[1]), "v"(abc[2]), "v"(abc[3]), "v"(abc[4]), "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3]),
+          "v"(q[4]));
+#undef M_L
+#else
+    for (int l = 0; l < 5; ++l)
+        for (int u = 0; u < 7; ++u) m[u] = fma(dpp_row_bcast(abc[l], u), q[l], m[u]);
+#endif
+}
+
+// the control block of M in every lane: (M55, M65, M66) = lane 5's m5, m6 and lane 6's m6
+__device__ inline void fac_mww(double t[3], double m5, double m6) {
+    t[0] = t[1] = t[2] = 0.0;
+#ifndef PLAN_HOST_EMU
+    const double one = 1.0;
+    asm("s_nop 1\n\t" PF("%0", "%3", "%5", 5) PF("%1", "%4", "%5", 5) PF("%2", "%4", "%5", 6)
+        : "+&v"(t[0]), "+&v"(t[1]), "+&v"(t[2]) : "v"(m5), "v"(m6), "v"(one));
+#else
+    t[0] = fma(dpp_row_bcast(m5, 5), 1.0, t[0]);
+    t[1] = fma(dpp_row_bcast(m6, 5), 1.0, t[1]);
+    t[2] = fma(dpp_row_bcast(m6, 6), 1.0, t[2]);
+#endif
+}
+
+// column j of Pn = M_xx + Hwx' K: pn[i] += sum_r Hwx(r, i) K(r, j), Hwx(r, i) = m[5 + r] of lane i
+__device__ inline void fac_pn(double pn[5], double m5, double m6, double m7, const double kc[3]) {
+#ifndef PLAN_HOST_EMU
+#define PN_I(D, L) PF(D, "%5", "%8", L) PF(D, "%6", "%9", L) PF(D, "%7", "%10", L)
+    asm("s_nop 1\n\t" PN_I("%0", 0) PN_I("%1", 1) PN_I("%2", 2) PN_I("%3", 3) PN_I("%4", 4)
+        : "+&v"(pn[0]), "+&v"(pn[1]), "+&v"(pn[2]), "+&v"(pn[3]), "+&v"(pn[4])
+        : "v"(m5), "v"(m6), "v"(m7), "v"(kc[0]), "v"(kc[1]), "v"(kc[2]));
+#undef PN_I
+#else
+    for (int i = 0; i < 5; ++i) {
+        pn[i] = fma(dpp_row_bcast(m5, i), kc[0], pn[i]);
+        pn[i] = fma(dpp_row_bcast(m6, i), kc[1], pn[i]);
+        pn[i] = fma(dpp_row_bcast(m7, i), kc[2], pn[i]);
+    }
+#endif
+}
+
+// P column j = (Pn + Pn')(:, j) / 2: s[i] = 0.5 Pn(i, j) + sum_r Pn(r, i) sel[r] with sel[r] = 0.5 on lane r
+__device__ inline void fac_sym(double s[5], const double pn[5], const double sel[5]) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) s[i] = 0.5 * pn[i];
+#ifndef PLAN_HOST_EMU
+#define SY_I(D, L) PF(D, "%5", "%10", L) PF(D, "%6", "%11", L) PF(D, "%7", "%12", L) PF(D, "%8", "%13", L) \
+    PF(D, "%9", "%14", L)
+    asm("s_nop 1\n\t" SY_I("%0", 0) SY_I("%1", 1) SY_I("%2", 2) SY_I("%3", 3) SY_I("%4", 4)
+        : "+&v"(s[0]), "+&v"(s[1]), "+&v"(s[2]), "+&v"(s[3]), "+&v"(s[4])
+        : "v"(pn[0]), "v"(pn[1]), "v"(pn[2]), "v"(pn[3]), "v"(pn[4]), "v"(sel[0]), "v"(sel[1]), "v"(sel[2]),
+          "v"(sel[3]), "v"(sel[4]));
+#undef SY_I
+#else
+    for (int i = 0; i < 5; ++i)
+        for (int r = 0; r < 5; ++r) s[i] = fma(dpp_row_bcast(pn[r], i), sel[r], s[i]);
+#endif
+}
+
+// two components of the co-state's control rhs in every lane: h[r] += sum_l B(l, r) p_l (B uniform, p_l of lane l)
+__device__ inline void sol_h(double& h0, double& h1, double p, const double B0[5], const double B1[5]) {
+#ifndef PLAN_HOST_EMU
+    asm("s_nop 1\n\t" PF("%0", "%2", "%3", 0) PF("%1", "%2", "%8", 0) PF("%0", "%2", "%4", 1) PF("%1", "%2", "%9", 1)
+        PF("%0", "%2", "%5", 2) PF("%1", "%2", "%10", 2) PF("%0", "%2", "%6", 3) PF("%1", "%2", "%11", 3)
+        PF("%0", "%2", "%7", 4) PF("%1", "%2", "%12", 4)
+        : "+&v"(h0), "+&v"(h1)
+        : "v"(p), "v"(B0[0]), "v"(B0[1]), "v"(B0[2]), "v"(B0[3]), "v"(B0[4]), "v"(B1[0]), "v"(B1[1]), "v"(B1[2]),
+          "v"(B1[3]), "v"(B1[4]));
+#else
+    for (int l = 0; l < 5; ++l) {
+        const double pl = dpp_row_bcast(p, l);
+        h0 = fma(pl, B0[l], h0);
+        h1 = fma(pl, B1[l], h1);
+    }
+#endif
+}
+
+// the feedback controls in every lane: w[r] += sum_l K(r, l) x_l (K uniform, x_l of lane l)
+__device__ inline void sol_w(double w[3], double x, const double K[15]) {
+#ifndef PLAN_HOST_EMU
+#define W_L(L, A, B, C) PF("%0", "%3", A, L) PF("%1", "%3", B, L) PF("%2", "%3", C, L)
+    asm("s_nop 1\n\t" W_L(0, "%4", "%9", "%14") W_L(1, "%5", "%10", "%15") W_L(2, "%6", "%11", "%16")
+        W_L(3, "%7", "%12", "%17") W_L(4, "%8", "%13", "%18")
+        : "+&v"(w[0]), "+&v"(w[1]), "+&v"(w[2])
+        : "v"(x), "v"(K[0]), "v"(K[1]), "v"(K[2]), "v"(K[3]), "v"(K[4]), "v"(K[5]), "v"(K[6]), "v"(K[7]), "v"(K[8]),
+          "v"(K[9]), "v"(K[10]), "v"(K[11]), "v"(K[12]), "v"(K[13]), "v"(K[14]));
+#undef W_L
+#else
+    for (int l = 0; l < 5; ++l) {
+        const double xl = dpp_row_bcast(x, l);
+        for (int r = 0; r < 3; ++r) w[r] = fma(xl, K[5 * r + l], w[r]);
+    }
+#endif
+}
+
+// LQ solve over the wave with zero initial state and homogeneous dynamics: stage linear terms at ogl -> odz
+// (the caller syncs before reading odz).  Backward: p_{k} = gx_k + A_k' p_{k+1} + K_k' h_k with h = gw + B' p
+// (lane i: p_i), kk_k = -(L D L')^-1 h_k stored by lane 0; forward: w = kk + K x, x <- A x + B w (lane i: x_i).
+// oracle solve_core().
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
-    const int N = X.N;
+    const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
-    const int me = X.ln < 5 ? X.ln : 0;
-    double p[5];
+    const Layout& Y = X.Y;
+    if (REC_LANES(ln)) {
+        const int me = (ln & 15) < 5 ? (ln & 15) : 4;
+        double p = (ln & 15) < 5 ? L[ogl + ZS * N + me] : 0.0;
+        for (int k = N - 1; k >= 0; --k) {
+            double B0[5], B1[5], Lc[6], Ac[5], Kc[3];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) p[i] = L[ogl + ZS * N + i];
-    BwdRec cur, nxt;
-    load_bwd(X, ogl, N - 1, me, cur);
-    for (int k = N - 1; k >= 0; --k) {
-        load_bwd(X, ogl, k > 0 ? k - 1 : 0, me, nxt);
-        SCHED_FENCE();
-        double h[3];
-        {
-            double v = cur.gw[0];
+            for (int l = 0; l < 5; ++l) {
+                B0[l] = L[Y.oB + 10 * k + 2 * l];
+                B1[l] = L[Y.oB + 10 * k + 2 * l + 1];
+                Ac[l] = L[Y.oA + 25 * k + 5 * l + me];
+            }
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v = fma(cur.B0[l], p[l], v);
-            h[0] = v;
-            v = cur.gw[1];
+            for (int i = 0; i < 6; ++i) Lc[i] = L[Y.oL + 6 * k + i];
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v = fma(cur.B1[l], p[l], v);
-            h[1] = v;
+            for (int r = 0; r < 3; ++r) Kc[r] = L[Y.oK + 15 * k + 5 * r + me];
+            double h0 = L[ogl + ZS * k + 5], h1 = L[ogl + ZS * k + 6];
+            const double h2 = L[ogl + ZS * k + 7], gx = L[ogl + ZS * k + me];
+            sol_h(h0, h1, p, B0, B1);
+            double t[3] = {-h0, -h1, -h2};
+            chol3_solve(Lc, t);
+            if (ln == 0)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) L[odz + ZS * k + 5 + i] = t[i];
+            if (k > 0) {
+                double v = gx;
+                dot5_lanes(v, p, Ac);
+                v = fma(Kc[0], h0, v);
+                v = fma(Kc[1], h1, v);
+                v = fma(Kc[2], h2, v);
+                p = v;
+            }
         }
-        h[2] = cur.gw[2];
-        double t[3] = {-h[0], -h[1], -h[2]};
-        chol3_solve(cur.Lc, t);
-        if (X.ln == 0)
-#pragma unroll
-            for (int i = 0; i < 3; ++i) L[odz + ZS * k + 5 + i] = t[i];
-        if (k > 0) {
-            double v = cur.gx;
-#pragma unroll
-            for (int l = 0; l < 5; ++l) v = fma(cur.Acol[l], p[l], v);
-#pragma unroll
-            for (int l = 0; l < 3; ++l) v = fma(cur.Kcol[l], h[l], v);
-#pragma unroll
-            for (int i = 0; i < 5; ++i) p[i] = bcast(v, i);
-        }
-        cur = nxt;
     }
-    // the forward pass reads the control parts just stored
+    // the forward pass reads the feed-forward terms just stored
     sync();
-    double x[5] = {0, 0, 0, 0, 0};
-    FwdRec fc, fn;
-    load_fwd(X, 0, me, fc);
-    for (int k = 0; k < N; ++k) {
-        load_fwd(X, k + 1 < N ? k + 1 : k, me, fn);
-        SCHED_FENCE();
-        double w[3];
+    if (REC_LANES(ln)) {
+        const int me = (ln & 15) < 5 ? (ln & 15) : 4;
+        double x = 0.0;
+        for (int k = 0; k < N; ++k) {
+            double K[15], Ar[5], w[3];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            double v = L[odz + ZS * k + 5 + i];
+            for (int i = 0; i < 15; ++i) K[i] = L[Y.oK + 15 * k + i];
 #pragma unroll
-            for (int l = 0; l < 5; ++l) v = fma(fc.K[5 * i + l], x[l], v);
-            w[i] = v;
+            for (int l = 0; l < 5; ++l) Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
+            const double b0 = L[Y.oB + 10 * k + 2 * me], b1 = L[Y.oB + 10 * k + 2 * me + 1];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) w[r] = L[odz + ZS * k + 5 + r];
+            sol_w(w, x, K);
+            double xn = 0.0;
+            dot5_lanes(xn, x, Ar);
+            xn = fma(b0, w[0], xn);
+            xn = fma(b1, w[1], xn);
+            // stage k overwritten after every lane has read its feed-forward terms (program order within the
+            // wave; the emulation's broadcasts above are barriers)
+            if (ln < 5) L[odz + ZS * k + ln] = x;
+            if (ln == 0)
+#pragma unroll
+                for (int r = 0; r < 3; ++r) L[odz + ZS * k + 5 + r] = w[r];
+            x = xn;
         }
-        double v = 0.0;
+        if (ln < 5) L[odz + ZS * N + ln] = x;
+        if (ln == 0)
 #pragma unroll
-        for (int l = 0; l < 5; ++l) v = fma(fc.Arow[l], x[l], v);
-#pragma unroll
-        for (int l = 0; l < 2; ++l) v = fma(fc.Brow[l], w[l], v);
-        // stage k overwritten after every lane has read its control part (the broadcast orders that)
-        double xn[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) xn[i] = bcast(v, i);
-        if (X.ln == 0) {
-#pragma unroll
-            for (int i = 0; i < 5; ++i) L[odz + ZS * k + i] = x[i];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) L[odz + ZS * k + 5 + i] = w[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 5; ++i) x[i] = xn[i];
-        fc = fn;
-    }
-    if (X.ln == 0) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) L[odz + ZS * N + i] = x[i];
-#pragma unroll
-        for (int i = 5; i < NZ; ++i) L[odz + ZS * N + i] = 0.0;
+            for (int i = 5; i < NZ; ++i) L[odz + ZS * N + i] = 0.0;
     }
 }
 
-// [A_k | B_k] (5 x 7: the state and the two control columns; the slack enters no dynamics) at (l, j)
-__device__ inline double ab_at(const Ctx& X, int k, int l, int j) {
-    return j < 5 ? X.L[X.Y.oA + 25 * k + 5 * l + j] : X.L[X.Y.oB + 10 * k + 2 * l + (j - 5)];
-}
-
-// entry (u, w) of stage k's factorisation Hessian: the stored value at the rows' entries, else H + delta I
-// (the same sums stage_hess_par forms)
-__device__ inline double ht_at(const Ctx& X, int k, int u, int w) {
-    const int sl = hs_slot(u, w);
-    if (sl >= 0) return X.L[X.Y.oHS + 8 * k + sl];
-    const double h = X.L[X.Y.oH + HSTR * k + hidx(u, w)];
-    return (u == w && u < (k < X.N ? NZ : 5)) ? h + X.delta : h;
-}
-
-// Riccati factorisation of the HT stage Hessians over the wave (uniform result: false when a control
-// pivot is not positive, or the final chunk's terminal system is singular).  Per stage, backwards:
-//   M = HT + [A B 0]' P [A B 0]  (xx, wx, ww)       49 lanes, one entry each (the column of P [A B] it
-//                                                   needs formed in the lane)
-//   Mww = L L' (every lane), K = -Mww^-1 Mwx        5 lanes store one gain column each
-//   P <- sym(Mxx + Mwx' K)                          25 lanes (forming the two gain columns they need)
-// two wave barriers per stage; every entry is formed by the same operations in the same order as the
-// recursion on one lane (round-4 first cut), so the rounding is the same, and the chain per stage is ~50
-// dependent FP64 operations instead of ~1100 issued on one lane.
+// Riccati factorisation of the HT stage Hessians (uniform result: false when a control pivot is not positive,
+// or the final chunk's terminal system is singular).  Per stage, backwards, lane j (oracle factor()):
+//   q = P [A B](:, j)                        25 broadcast FMAs (P(i, l) from lane l)
+//   m = HT(:, j) + [A B]' q                  35 broadcast FMAs ([A B](l, u) from lane u)
+//   Mww = L D L' (every lane, from lanes 5 and 6), K(:, j) = -Mww^-1 Mwx(:, j), lanes 0..4 store it
+//   P(:, j) <- sym(Mxx + Mwx' K)(:, j)       15 + 25 broadcast FMAs
+// The slack has no dynamics (B's third column is zero), so its rows of Mww and Mwx are HT's: the third pivot
+// is HT(7, 7) and the factor's (2, 0), (2, 1) entries are exact zeros, as in the oracle's chol3 of the same
+// matrix.  Column j of HT comes from the packed H (+ delta on the diagonal) except at the 8 entries rows
+// touch, which stage_hess_par stored in HS (ht_at).
 __device__ bool factor_par(const Ctx& X) {
     const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
-    ldsd* P = L + Y.oWK;
-    ldsd* M = P + 25;
-    if (ln < 25) P[ln] = ht_at(X, N, ln / 5, ln % 5);
-    sync();
-    for (int k = N - 1; k >= 0; --k) {
-        if (ln < 49) {
-            int u, w;
-            if (ln < 25) { u = ln / 5; w = ln % 5; }
-            else if (ln < 40) { u = 5 + (ln - 25) / 5; w = (ln - 25) % 5; }
-            else { u = 5 + (ln - 40) / 3; w = 5 + (ln - 40) % 3; }
-            double m = ht_at(X, k, u, w);
-            if (u < 7 && w < 7) {
-                double pab[5];                      // column w of P [A | B], formed in this lane
+    double okv = 1.0;
+    if (REC_LANES(ln)) {
+        const int j = (ln & 15) < 7 ? (ln & 15) : 7;
+        // per-lane address of HT(u, j): HS slot or packed H entry; dg: the diagonal entries H + delta I adds to
+        int hoff[8];
+        bool hsl[8];
 #pragma unroll
-                for (int i = 0; i < 5; ++i) {
-                    double v = 0.0;
-#pragma unroll
-                    for (int l = 0; l < 5; ++l) v = fma(P[5 * i + l], ab_at(X, k, l, w), v);
-                    pab[i] = v;
-                }
-#pragma unroll
-                for (int l = 0; l < 5; ++l) m = fma(ab_at(X, k, l, u), pab[l], m);
-            }
-            M[8 * u + w] = m;
+        for (int u = 0; u < 8; ++u) {
+            const int sl = hs_slot(u, j);
+            hsl[u] = sl >= 0;
+            hoff[u] = sl >= 0 ? sl : hidx(u, j);
         }
-        sync();
-        double Hww[3][3], Lc[6];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) Hww[r][c] = M[8 * (5 + r) + 5 + c];
-        if (!chol3(Hww, Lc)) return false;
-        // gain column j = -Mww^-1 Mwx(:, j): lanes 0..4 store theirs; the P lanes form the two they need
-        auto gain = [&](int j, double col[3]) {
-            col[0] = -M[8 * 5 + j];
-            col[1] = -M[8 * 6 + j];
-            col[2] = -M[8 * 7 + j];
-            chol3_solve(Lc, col);
+        const double dg1 = (j == 1) ? 1.0 : 0.0, dg2 = (j == 2) ? 1.0 : 0.0;
+        auto ht = [&](int k, int u) {
+            const double v = hsl[u] ? L[Y.oHS + 8 * k + hoff[u]] : L[Y.oH + HSTR * k + hoff[u]];
+            // ht_at: (u == w && u < nv) ? h + delta : h for the non-slot diagonal entries (1, 1), (2, 2)
+            return u == 1 ? fma(dg1, X.delta, v) : (u == 2 ? fma(dg2, X.delta, v) : v);
         };
-        if (ln < 5) {
-            double col[3];
-            gain(ln, col);
-            L[Y.oK + 15 * k + ln] = col[0];
-            L[Y.oK + 15 * k + 5 + ln] = col[1];
-            L[Y.oK + 15 * k + 10 + ln] = col[2];
-        } else if (ln < 11) {
-            L[Y.oL + 6 * k + ln - 5] = Lc[ln - 5];
-        }
-        if (k > 0 && ln < 25) {
-            const int i = ln / 5, j = ln % 5;
-            double ki[3], kj[3];
-            gain(i, ki);
-            gain(j, kj);
-            double a = M[8 * i + j], b = M[8 * j + i];
+        double Pc[5], sel[5];
 #pragma unroll
-            for (int l = 0; l < 3; ++l) a = fma(M[8 * (5 + l) + i], kj[l], a);
-#pragma unroll
-            for (int l = 0; l < 3; ++l) b = fma(M[8 * (5 + l) + j], ki[l], b);
-            P[ln] = 0.5 * (a + b);
+        for (int i = 0; i < 5; ++i) {
+            Pc[i] = ht(N, i);
+            sel[i] = (j == i) ? 0.5 : 0.0;
         }
-        sync();
+        for (int k = N - 1; k >= 0; --k) {
+            double abc[5], m[8];
+#pragma unroll
+            for (int l = 0; l < 5; ++l)
+                abc[l] = j < 5 ? L[Y.oA + 25 * k + 5 * l + j] : (j < 7 ? L[Y.oB + 10 * k + 2 * l + (j - 5)] : 0.0);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) m[u] = ht(k, u);
+            const double h77 = L[Y.oHS + 8 * k + 7];
+            double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+            fac_pab(q, Pc, abc);
+            fac_m(m, abc, q);
+            double t[3], Lc[6];
+            fac_mww(t, m[5], m[6]);
+            // chol3 of [[M55, ., .], [M65, M66, .], [0, 0, HT77]] (oracle chol3, same operations)
+            const double d0 = t[0];
+            if (!(d0 > 0.0)) { okv = 0.0; break; }
+            Lc[0] = 1.0 / d0;
+            Lc[1] = t[1] * Lc[0];
+            const double d1 = t[2] - Lc[1] * t[1];
+            if (!(d1 > 0.0)) { okv = 0.0; break; }
+            Lc[2] = 1.0 / d1;
+            Lc[3] = 0.0;
+            Lc[4] = 0.0;
+            if (!(h77 > 0.0)) { okv = 0.0; break; }
+            Lc[5] = 1.0 / h77;
+            double kc[3] = {-m[5], -m[6], -m[7]};
+            chol3_solve(Lc, kc);
+            if (ln < 5)
+#pragma unroll
+                for (int r = 0; r < 3; ++r) L[Y.oK + 15 * k + 5 * r + ln] = kc[r];
+            if (ln == 0)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) L[Y.oL + 6 * k + i] = Lc[i];
+            if (k > 0) {
+                double pn[5] = {m[0], m[1], m[2], m[3], m[4]};
+                fac_pn(pn, m[5], m[6], m[7], kc);
+                fac_sym(Pc, pn, sel);
+            }
+        }
+        if (ln >= 8) okv = 1.0;          // the emulation's replicas of the recursion lanes
     }
+    if (wmin(okv) == 0.0) return false;
+    sync();
     if (X.fin) {
         for (int c = 0; c < 2; ++c) {
             for (int k = ln; k <= N; k += WAVE)
@@ -1131,30 +1214,29 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     sync();
 }
 
-// dynamics-feasible start at oz: dx_0 = xi0, dw = 0 (the state recursion one entry per lane on lanes 0..4,
-// broadcast by readlane; lane 0 stores)
+// dynamics-feasible start at oz: dx_0 = xi0, dw = 0 (lane i: x_i, the A x products broadcast by DPP; oracle
+// rollout())
 __device__ void rollout(const Ctx& X, int oz) {
     PHASE(PH_ROLLOUT);
-    const int N = X.N;
+    const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
-    const int me = X.ln < 5 ? X.ln : 0;
-    double x[5];
+    if (REC_LANES(ln)) {
+        const int me = (ln & 15) < 5 ? (ln & 15) : 4;
+        double x = X.xi0[me];
+        for (int k = 0; k <= N; ++k) {
+            if (ln < 5) L[oz + ZS * k + ln] = x;
+            if (ln == 0)
 #pragma unroll
-    for (int i = 0; i < 5; ++i) x[i] = X.xi0[i];
-    for (int k = 0; k <= N; ++k) {
-        if (X.ln == 0) {
+                for (int i = 5; i < NZ; ++i) L[oz + ZS * k + i] = 0.0;
+            if (k == N) break;
+            double Ar[5];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) L[oz + ZS * k + i] = x[i];
-#pragma unroll
-            for (int i = 5; i < NZ; ++i) L[oz + ZS * k + i] = 0.0;
+            for (int l = 0; l < 5; ++l) Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
+            double v = L[Y.oC + 5 * k + me];
+            dot5_lanes(v, x, Ar);
+            x = v;
         }
-        if (k == N) break;
-        double v = L[Y.oC + 5 * k + me];
-#pragma unroll
-        for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * me + l] * x[l];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) x[i] = bcast(v, i);
     }
     sync();
 }
@@ -1541,30 +1623,23 @@ __device__ void multipliers(Ctx& X) {
         for (int u = 0; u < 5; ++u) L[Y.oGL + ZS * k + u] = g[u];
     }
     sync();
-    // co-states: PI[k] = pi_{k+1} (one entry per lane on lanes 0..4, broadcast by readlane; lane 0 stores)
-    {
-        const int me = X.ln < 5 ? X.ln : 0;
-        double pi[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) pi[i] = L[Y.oGL + ZS * N + i];
-        if (X.fin) {
-            pi[0] += X.nu[0];
-            pi[4] += X.nu[1];
-        }
+    // co-states: PI[k] = pi_{k+1} (lane i: pi_i, the A' pi products broadcast by DPP)
+    if (REC_LANES(X.ln)) {
+        const int ln = X.ln, me = (ln & 15) < 5 ? (ln & 15) : 4;
+        double pi = L[Y.oGL + ZS * N + me];
+        if (X.fin) pi += me == 0 ? X.nu[0] : (me == 4 ? X.nu[1] : 0.0);
         for (int k = N - 1; k >= 0; --k) {
-            if (X.ln == 0)
-#pragma unroll
-                for (int i = 0; i < 5; ++i) L[Y.oPI + 5 * k + i] = pi[i];
+            if (ln < 5) L[Y.oPI + 5 * k + ln] = pi;
             if (k > 0) {
+                double Ac[5];
+#pragma unroll
+                for (int l = 0; l < 5; ++l) Ac[l] = L[Y.oA + 25 * k + 5 * l + me];
                 double v = L[Y.oGL + ZS * k + me];
-#pragma unroll
-                for (int l = 0; l < 5; ++l) v += L[Y.oA + 25 * k + 5 * l + me] * pi[l];
-#pragma unroll
-                for (int i = 0; i < 5; ++i) pi[i] = bcast(v, i);
+                dot5_lanes(v, pi, Ac);
+                pi = v;
             }
         }
     }
-    sync();
     // y_k = D1_k^-T pi_{k+1} (stage-parallel; D1 at the iterate ZB)
     for (int k = X.ln; k < N; k += WAVE) {
         double xa[5], xb[5], D1[25], D1t[25], y[5];
@@ -1686,7 +1761,7 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
     double last = INFINITY, mu_m = 0.0, hf[LS_MEMORY], hv[LS_MEMORY];
     int nh = 0;
     for (int it = 0; it < X.P.sqp_iters; ++it, ++since) {
-        bool exact = last <= EXACT_STEP;
+        bool exact = last <= EXACT_STEP || it >= EXACT_AFTER;
         int rc = -1;
         for (;;) {
             if (X.dbg & 16) (void)build_qp(X, frozen, exact);
@@ -1795,6 +1870,7 @@ struct KArgs {
     DevRoute R;
     plan_params P;
     int B, Nmax, Nfixed, dbg;
+    const int* order;          // dispatch order (plan_order_kernels): workgroup w solves chunk order[w]; NULL = w
     const int* N;
     const double *x0, *st;
     const int* fin;
@@ -1804,7 +1880,7 @@ struct KArgs {
 
 __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
     PLAN_LDS_DECL;
-    const int b = blockIdx.x;
+    const int b = a.order ? a.order[blockIdx.x] : (int)blockIdx.x;
     Ctx X;
     X.R = a.R;
     X.P = a.P;
@@ -1958,6 +2034,46 @@ __global__ void __launch_bounds__(WAVE) plan_loop_kernel(LArgs a) {
         sync();          // every lane has its next start before the next chunk rewrites the block
     }
     if (X.ln == 0) a.nchunks[b] = err ? -(n + 1) : n;
+}
+
+// Longest-first dispatch (a scheduling hint; every chunk's result is independent of the order).  A launch
+// lasts as long as its slowest chunk, and the slow chunks are the ones whose path the vehicle cannot follow
+// at the speed limit: a route curvature beyond the curvature bound, or one whose lateral acceleration at
+// the limit exceeds a_max (on traj3 a spike of |kappa| = 1 at s = 720 m makes chunks nearby need 50-100 SQP
+// iterations and up to 2000 interior-point iterations).  Score of chunk b: the largest of |kappa| / k_max and
+// |kappa| vmax^2 / a_max over ORDER_SAMPLES points of [s0, s0 + 1.5 (s_target - s0)]; the chunks are
+// dispatched by score bucket, highest first (ORDER_BUCKETS power-of-two buckets from 1/4 up), so the
+// expensive ones start with the launch instead of wherever their index puts them.
+constexpr int ORDER_SAMPLES = 32;
+constexpr int ORDER_BUCKETS = 8;
+__device__ inline int order_bucket(const DevRoute& R, const plan_params& P, double s0, double st) {
+    double sc = 0.0;
+    const double kb = fmax(fabs(P.k_min), fabs(P.k_max));
+    for (int i = 0; i < ORDER_SAMPLES; ++i) {
+        const double s = s0 + (1.5 * (st - s0)) * ((double)i / (ORDER_SAMPLES - 1));
+        const double k = fabs(route_kappa(R, s, nullptr, nullptr)), vm = route_vmax(R, s);
+        sc = fmax(sc, fmax(k / kb, k * vm * vm / P.a_max));
+    }
+    // bucket 0 = highest: score >= 16; then [8, 16), ..., [0.25, 0.5); the last bucket holds the rest
+    int q = 0;
+    for (double th = 16.0; q < ORDER_BUCKETS - 1 && !(sc >= th); th *= 0.5) ++q;
+    return q;
+}
+__global__ void plan_order_count_kernel(DevRoute R, plan_params P, int B, const double* x0, const double* st,
+                                        int* bucket, int* cnt) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int q = order_bucket(R, P, x0[5 * (size_t)b], st[b]);
+    bucket[b] = q;
+    atomicAdd(&cnt[q], 1);
+}
+__global__ void plan_order_scatter_kernel(int B, const int* bucket, const int* cnt, int* cur, int* order) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int q = bucket[b];
+    int off = 0;
+    for (int i = 0; i < q; ++i) off += cnt[i];
+    order[off + atomicAdd(&cur[q], 1)] = b;
 }
 
 __global__ void route_eval_kernel(DevRoute R, int n, const double* s, double* k, double* dk, double* vm) {

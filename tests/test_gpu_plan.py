@@ -4,7 +4,10 @@ importable here); the oracle is pinned by tests/test_plan_oracle.py (scipy SLSQP
 committed planner outputs, the reference_trajectory_check goldens).
 
 Tolerances: chunks that both sides solve to convergence (status ok / frozen limits) agree to 1e-8 abs on
-X, U, S (both converge to the same KKT point to sqp_tol 1e-9); statuses agree on >= 95% of the chunks.
+X, U, S (both converge to the same KKT point to sqp_tol 1e-9; measured <= 8e-13); statuses agree on >= 99% of
+the chunks (measured 0.996-1.000), and both sides converge on >= 95% of the chunks whose QP is not infeasible
+(the oracle's PLAN_QP_FAILED: e.g. 15 of the 256 traj1 N = 10 chunks start with a curvature outside the
+k bounds that 3 s cannot undo, or must stop within the horizon).
 """
 import numpy as np
 import pytest
@@ -46,8 +49,10 @@ def compare(label, r, ro):
     print(f"{label}: B={len(both)} status agree {agree:.3f}, both converged {both.sum()}, max err {err[both].max():.1e}, "
           f"GPU statuses {np.bincount(r['status'], minlength=5).tolist()}, oracle {np.bincount(ro['status'], minlength=5).tolist()}, "
           f"sqp mean {r['sqp'].mean():.1f} max {r['sqp'].max()}")
-    assert agree >= 0.95, label
+    assert agree >= 0.99, label
     assert err[both].max() <= TOL, (label, np.flatnonzero(both & (err > TOL)))
+    feasible = ro["status"] != 2
+    assert both.sum() >= 0.95 * feasible.sum(), (label, int(both.sum()), int(feasible.sum()))
     return both
 
 
@@ -60,8 +65,7 @@ def test_chunks_vs_oracle(env, N, route):
     pl = mpcplan.Planner(r, mpcplan.default_params(N=N))
     g = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
     o = PO.PlanOracle(r).solve_batch(PO.default_params(N=N), wb["x0"], wb["s_target"], wb["is_final"], num_threads=16)
-    both = compare(f"N={N} {route}", g, o)
-    assert both.mean() >= 0.7
+    compare(f"N={N} {route}", g, o)
     pl.close()
 
 
@@ -145,7 +149,9 @@ def test_horizon_extremes_vs_oracle(env, N):
     err = max((float(np.abs(g[k][both] - o[k][both]).max()) for k in ("X", "U", "S")), default=0.0) if both.any() else 0.0
     print(f"N={N}: status agree {agree:.3f}, both converged {int(both.sum())}/24, max err {err:.1e}, "
           f"GPU statuses {np.bincount(g['status'], minlength=5).tolist()}")
-    assert agree >= 0.9
+    assert agree >= 0.99
+    if N > 1:         # N = 1 (0.3 s for a 20 m chunk) converges on neither side: statuses agree, plans unchecked
+        assert both.sum() >= 0.95 * (o["status"] != 2).sum()
     assert err <= TOL
     assert np.isfinite(g["X"]).all()
 
@@ -238,3 +244,43 @@ def test_device_loop_equals_round_loop(env, capsys):
     with capsys.disabled():
         print(f"\ndevice loop = round loop on 40 plans, chunks per plan "
               f"{min(len(q['statuses']) for q in sd)}-{max(len(q['statuses']) for q in sd)}")
+
+
+def test_longest_first_order_changes_nothing(env, monkeypatch):
+    """plan_solve_chunks_device dispatches the chunks by a route-curvature score, highest first (plan_order_*_
+    kernel, a scheduling hint): every chunk's plan, status and counts equal the index-order launch's bit for bit
+    (PLAN_ORDER=0 at plan_create), including batches on two streams of one context at once."""
+    import torch
+    mpcplan, PO, W = env
+    r = W.plan_route("traj3")
+    wb = W.plan_batch(r, 14, 2048, seed=21, final_frac=0.1)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    x0, st, fin = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32)
+    B = 2048
+
+    def run(pl, stream):
+        X = torch.empty((B, 15, 5), dtype=torch.float64, device=dev)
+        o = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3)]
+        pl.solve_chunks_device(B, 14, 0, x0.data_ptr(), st.data_ptr(), fin.data_ptr(), X.data_ptr(), 0, 0,
+                               *[a.data_ptr() for a in o], stream=stream.cuda_stream)
+        return X, o
+    monkeypatch.setenv("PLAN_ORDER", "0")
+    plain = mpcplan.Planner(r, mpcplan.default_params(N=14))
+    monkeypatch.setenv("PLAN_ORDER", "1")
+    ordered = mpcplan.Planner(r, mpcplan.default_params(N=14))
+    s0, s1 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s0.wait_stream(torch.cuda.current_stream(dev))
+    s1.wait_stream(torch.cuda.current_stream(dev))
+    Xa, oa = run(plain, s0)
+    Xb, ob = run(ordered, s0)
+    Xc, oc = run(ordered, s1)          # the same context on a second stream at the same time
+    torch.cuda.synchronize(dev)
+    for Xo, oo in ((Xb, ob), (Xc, oc)):
+        assert torch.equal(Xo, Xa)
+        for a, b in zip(oo, oa):
+            assert torch.equal(a, b)
+    print(f"\nordered dispatch == index order on {B} traj3 chunks; statuses "
+          f"{np.bincount(oa[0].cpu().numpy(), minlength=5).tolist()}")
+    plain.close()
+    ordered.close()

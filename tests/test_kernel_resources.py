@@ -6,9 +6,10 @@ counts), so a full unroll that silently fails in a horizon-specialised kernel wo
 turn the unrolled ping-pong records into dynamically indexed arrays and show up as scratch.  Pinned here:
   - the C2 path (crossover kernel + interior-point kernel, N = 20, no obstacles) uses no scratch at all;
   - no crossover kernel uses scratch;
-  - the horizon-specialised single-QP kernels (split pair and one-launch, NT = 20, 30, 40) stay at the
-    small spills measured in round 3 (<= 128 B per lane; they were 148-412 B before the split kernels lost
-    their runtime SQP loop);
+  - the horizon-specialised single-QP kernels (split pair and one-launch, NT = 20, 30, 40) stay at small
+    spills (<= 160 B per lane: 116 B in round 3; 148 B since the round-5 interior-point checkpoint keeps the
+    iterate live across its polish, measured C5 -5% and C3 -2% in a two-order A/B; they
+    were 148-412 B before the split kernels lost their runtime SQP loop);
   - no kernel exceeds 512 B per lane.
 """
 import os
@@ -59,5 +60,5 @@ def test_specialised_single_qp_kernels_spill_little(kernels):
     for key, k in kernels.items():
         gl, obs, mode, nt = key
         if nt > 0 and mode in (1, 2, 3):
-            assert k["scratch"] <= 128, (key, k)
+            assert k["scratch"] <= 160, (key, k)
         assert k["scratch"] <= 512, (key, k)

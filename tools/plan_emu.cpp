@@ -61,6 +61,14 @@ static inline double bcast(double v, int src) {
     pthread_barrier_wait(&g_bar);
     return r;
 }
+// DPP row_newbcast: every lane gets lane L of its 16-lane row
+static inline double dpp_row_bcast(double v, int L) {
+    g_xd[threadIdx.x] = v;
+    pthread_barrier_wait(&g_bar);
+    const double r = g_xd[(threadIdx.x & ~15u) + (unsigned)L];
+    pthread_barrier_wait(&g_bar);
+    return r;
+}
 #define PLAN_HOST_EMU 1
 
 #include "../safe-autonomous-driving-mpc_amd/csrc/plan_kernel.h"
