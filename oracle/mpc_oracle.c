@@ -841,33 +841,8 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
     }
 
     double X[MAXN + 1][5];
-    const int start2 = getenv("ORC_START2_N") && N >= atoi(getenv("ORC_START2_N"));
     double bscale = 0.0, rowc = 0.0;
-    if (start2) {
-        memset(S->du, 0, sizeof(double) * 2 * N);
-        for (int k = 1; k <= N; ++k)
-            for (int j = 0; j < NROW; ++j) {
-                if (!Q->on[j]) continue;
-                const double r0 = -Q->b[k][j];
-                const double xi = (r0 < 0 ? -r0 : 0.0) + 1e-1;
-                const double sv = r0 + xi;
-                const double lam = 1000.0 / sv < 0.5 * rho ? 1000.0 / sv : 0.5 * rho;
-                S->xi[k][j] = xi;
-                S->s[k][j] = sv;
-                S->lam[k][j] = lam;
-                S->nu[k][j] = rho - lam;
-                rowc += S->s[k][j] * S->lam[k][j] + S->xi[k][j] * S->nu[k][j];
-                if (fabs(Q->b[k][j]) > bscale) bscale = fabs(Q->b[k][j]);
-            }
-        const double mrow2 = rowc / (double)(2 * nsoft * N);
-        for (int t = 0; t < N; ++t)
-            for (int j = 0; j < NBOX; ++j) {
-                const double r0 = -Q->bb[t][j];
-                S->sb[t][j] = r0 > 1.0 ? r0 : 1.0;
-                S->lb[t][j] = mrow2 / S->sb[t][j];
-                if (fabs(Q->bb[t][j]) > bscale) bscale = fabs(Q->bb[t][j]);
-            }
-    } else {
+    {
     /* Interior-point start (round 3): centred at the unconstrained optimum of QP(ubar) (one Riccati
      * factorisation and solve without rows), or at du = 0 when the soft rows are less violated there.  Each soft row with value r = C x - b there gets slack
      * max(r, 0) + START_SHIFT and elastic slack max(-r, 0) + START_SHIFT, and the multiplier pair on the

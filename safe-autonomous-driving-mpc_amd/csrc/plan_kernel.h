@@ -134,6 +134,8 @@ __host__ __device__ Layout make_layout(int Nmax) {
 
 // phases of the diagnostic build
 enum { PH_OTHER, PH_BUILD, PH_HESS, PH_FACTOR, PH_SOLVE, PH_IPM, PH_EQP, PH_MULT, PH_LSEARCH, PH_ROLLOUT, PH_COUNT };
+// call counters of the diagnostic build (slots after the phases)
+enum { PH_NFACTOR = PH_COUNT, PH_NSOLVE, PH_NSLOTS };
 
 // scalar slots (oSC + ...)
 enum { SC_DELTA, SC_NU0, SC_NU1, SC_EM0, SC_EM1, SC_EM2, SC_EM3, SC_FLAG };
@@ -512,8 +514,14 @@ struct PhScope {
     }
 };
 #define PHASE(p) PhScope ph_scope_(X, p)
+// calls of a phase (factorisations, solves), so that tools/plan_phase.py can report cycles per call and stage
+#define PROF_COUNT(p)                                                                        \
+    do {                                                                                     \
+        if (X.ln == 0) *(PLAN_LDS_AS unsigned long long*)(X.L + X.Y.oSC + 16 + (p)) += 1ull; \
+    } while (0)
 #else
 #define PHASE(p)
+#define PROF_COUNT(p)
 #endif
 
 __device__ inline bool act_bit(const Ctx& X, int o, int k, int j) {
@@ -1181,6 +1189,7 @@ __device__ bool factor_reg(Ctx& X, int mode) {
             ok = factor_par(X);
             sync();
         }
+        PROF_COUNT(PH_NFACTOR);
         if (ok) return true;
         if (X.delta >= DELTA_MAX) return false;
         X.delta = X.delta > 0.0 ? 10.0 * X.delta : DELTA0;
@@ -1190,6 +1199,7 @@ __device__ bool factor_reg(Ctx& X, int mode) {
 // full solve (GL filled and synced): DZ; meets E dz_N = rE exactly (final chunk); X.nu = terminal forces
 __device__ void solve(Ctx& X, const double rE[2]) {
     PHASE(PH_SOLVE);
+    PROF_COUNT(PH_NSOLVE);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const int N = X.N;
@@ -1944,7 +1954,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
 #ifdef PLAN_PROF
     if (X.ln == 0) {
         *(PLAN_LDS_AS unsigned long long*)(lds_p(X) + X.Y.oSC + 16 + PH_OTHER) = __builtin_amdgcn_s_memtime() - t_total0;
-        for (int i = 0; i < PH_COUNT; ++i)
+        for (int i = 0; i < PH_NSLOTS; ++i)
             atomicAdd(&g_plan_prof[i], *(PLAN_LDS_AS unsigned long long*)(lds_p(X) + X.Y.oSC + 16 + i));
         atomicAdd(&g_plan_prof[15], 1ull);
     }

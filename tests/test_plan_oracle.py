@@ -100,6 +100,61 @@ def test_oracle_optimum_matches_slsqp(env, N, final):
     assert checked >= 2
 
 
+def _slsqp_from(job):
+    """Worker of test_oracle_optimum_matches_slsqp_bench_mix: SLSQP (analytic Jacobians, ftol 1e-14) on the
+    restated chunk NLP started at the oracle's answer z; returns (max |x - z|, SLSQP cost, cost at z, max |eq|,
+    min ineq)."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "safe-autonomous-driving-mpc_amd"), os.path.join(root, "oracle")]
+    import plan_ref as PR
+    import workloads as W
+    route, n, x0, st, fin, z = job
+    ch = PR.Chunk(W.plan_route(route), n, 0.3, x0, st, fin)
+    rt, _ = ch.slsqp(ftol=1e-14, maxiter=400, jac=True, z0=z)
+    return float(np.abs(rt.x - z).max()), float(rt.fun), float(ch.cost(z)), float(np.abs(ch.eq(z)).max()), \
+        float(ch.ineq(z).min())
+
+
+def test_oracle_optimum_matches_slsqp_bench_mix(env, capsys):
+    """The same check over the chunks bench.py's planner leg solves (workloads.plan_batch_ref on traj3: 20 m
+    chunks with the reference's horizon rule, N = 13..17, final chunks N = 25..32): for every horizon, four
+    chunks the oracle solves to convergence are KKT points of the restated NLP that scipy SLSQP (analytic
+    Jacobians, ftol 1e-14) started there does not leave (1e-6), at no lower cost.  (8 worker processes: the
+    N = 32 problems take ~10 s each.)"""
+    import multiprocessing as mp
+    from concurrent.futures import ProcessPoolExecutor
+    PO, PR, W = env
+    r = W.plan_route("traj3")
+    orc = PO.PlanOracle(r)
+    wb = W.plan_batch_ref(r, 2048, seed=7)
+    o = orc.solve_batch(PO.default_params(N=int(wb["N"].max())), wb["x0"], wb["s_target"], wb["is_final"], N=wb["N"],
+                        num_threads=8)
+    per_n, jobs = {}, []
+    for b in range(len(wb["N"])):
+        n = int(wb["N"][b])
+        if o["status"][b] != 0 or per_n.get(n, 0) >= 4:
+            continue
+        z = np.concatenate([o["X"][b][:n + 1].ravel(), o["U"][b][:n].ravel(), o["S"][b][:n]])
+        jobs.append(("traj3", n, wb["x0"][b], float(wb["s_target"][b]), bool(wb["is_final"][b]), z))
+        per_n[n] = per_n.get(n, 0) + 1
+    with ProcessPoolExecutor(8, mp_context=mp.get_context("spawn")) as ex:
+        res = list(ex.map(_slsqp_from, jobs))
+    worst = 0.0
+    for job, (d, fun, cost, eq, ineq) in zip(jobs, res):
+        assert eq <= 1e-9 and ineq >= -1e-9, job[:2]
+        assert d <= 1e-6, (job[:2], d)
+        assert fun >= cost - 1e-8, job[:2]
+        worst = max(worst, d)
+    finals = sorted({int(n) for n, f in zip(wb["N"], wb["is_final"]) if f})
+    with capsys.disabled():
+        print(f"\nbench mix: horizons {sorted(per_n)} (final-chunk horizons {finals}), chunks checked {len(jobs)}, "
+              f"largest SLSQP move {worst:.1e}")
+    assert all(per_n.get(n, 0) >= 4 for n in set(int(x) for x in wb["N"])), per_n
+    assert set(range(13, 18)) <= set(per_n) and set(range(25, 33)) <= set(per_n)
+
+
 def test_receding_horizon_loop_with_oracle_passes_check(env, capsys):
     """optimize_full_trajectory (:419-559) with the oracle as the chunk solver on a synthetic route: the planned
     trajectory reaches the destination, stops, and passes the restated reference_trajectory_check."""

@@ -16,7 +16,7 @@ import mpcplan
 mpcplan.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcplan_prof.so")
 import workloads as W
 
-PHASES = ["TOTAL", "build_qp", "stage_hess", "factor(lane0)", "solve", "ipm_rows", "eqp_rows", "multipliers",
+PHASES = ["TOTAL", "build_qp", "stage_hess", "factor", "solve", "ipm_rows", "eqp_rows", "multipliers",
           "line_search", "rollout"]
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 20
@@ -43,4 +43,10 @@ for B in [int(x) for x in Bs.split(",")]:
     print(f"ticks per chunk {tot / max(1, buf[15]):.3e}")
     for n, x in zip(PHASES, v):
         print(f"  {n:14s} {x / max(tot, 1) * 100:6.2f}%   {x / max(1, buf[15]):.3e} ticks/chunk", flush=True)
+    nf, ns = int(buf[len(PHASES)]), int(buf[len(PHASES) + 1])
+    if nf and ns:
+        # s_memtime ticks = shader cycles; factorisation and solve of N stages each (inclusive of the final chunk's
+        # two terminal-response solves inside a factorisation)
+        print(f"  factorisations {nf}: {v[3] / nf:.0f} cycles each = {v[3] / nf / N:.0f} per stage; solves {ns}: "
+              f"{v[4] / ns:.0f} cycles each = {v[4] / ns / N:.0f} per stage", flush=True)
     pl.close()
