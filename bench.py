@@ -466,20 +466,23 @@ def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_ego
 def executed_work(config):
     """Executed FP64 work of this config's dominant kernel from the last PMC pass over it (rocprofv3 --pmc
     SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64, SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES in their own
-    run: tools/gpu_f64_pmc.sh, summarised by tools/pmc_f64.py into profiles/r04_pmc_f64_<config>.csv).
+    run: tools/gpu_f64_pmc.sh, summarised by tools/pmc_f64.py into profiles/r<NN>_pmc_f64_<config>.csv, the
+    newest round's file).
     executed_frac = (2 FMA + MUL + ADD + TRANS) x 64 lanes / kernel time / 78.6 TF: an upper bound, since the
     recursions issue under narrowed exec masks; valu_busy = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES."""
     import csv
-    path = os.path.join(ROOT, "profiles", f"r04_pmc_f64_{config}.csv")
-    if not os.path.exists(path):
+    # the newest round's pass of this config (profiles/r<NN>_pmc_f64_<config>.csv)
+    cands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_pmc_f64_{config}.csv"))
+    if not cands:
         return {}
+    path = os.path.join(ROOT, "profiles", cands[-1])
     rows = list(csv.DictReader(open(path)))
     if not rows:
         return {}
     top = max(rows, key=lambda r: float(r.get("avg_duration_s") or 0.0))
     f = lambda r, k: float(r[k]) if r.get(k) not in (None, "") else None
     return {"executed_frac": f(top, "executed_frac_upper"), "valu_busy": f(top, "valu_busy"),
-            "kernel": top["kernel"], "source": f"profiles/r04_pmc_f64_{config}.csv",
+            "kernel": top["kernel"], "source": "profiles/" + cands[-1],
             "per_kernel": {r["kernel"]: {"executed_TFLOPs_upper": f(r, "executed_TFLOPs_upper"),
                                          "executed_frac_upper": f(r, "executed_frac_upper"),
                                          "valu_busy": f(r, "valu_busy"), "fp64_insts": f(r, "fp64_insts"),
@@ -492,8 +495,8 @@ def executed_work(config):
 def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
     """Offline planner: B chunk NLPs per GPU (workloads.plan_batch_ref: 20 m chunks at random
     positions of the route, each with the reference's own horizon rule, 10% final chunks), solved on the device
-    by libmpcplan, one launch per horizon (the chunks come sorted by N, so each launch sizes its LDS for its
-    own N) on one stream; `steps` timed passes over the batch after one warm-up, HIP events on that stream,
+    by libmpcplan, one launch per residency class of horizons (the chunks come sorted by N; a class's launch
+    sizes its LDS for its largest N, mpcplan.Planner.horizon_groups) on side streams; `steps` timed passes over the batch after one warm-up, HIP events on that stream,
     max over ranks.  On rank 0 also: the oracle (oracle/plan_oracle.c, OpenMP) and the restated reference
     path (scipy SLSQP on the chunk NLP, oracle/plan_ref.py) on bounded samples of the same chunks, and the
     GPU-vs-oracle agreement on the oracle's sample."""
@@ -514,16 +517,20 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
         raise RuntimeError(f"planner context on device {pl.device}, the rank's device is {dev.index}")
     t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
     x0, st, fin, Nd = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32), t(Nv, torch.int32)
+    # one launch per residency class (Planner.horizon_groups: the horizons whose own launches would keep the
+    # same chunks per CU share one launch sized for the largest, with per-chunk N), so each launch's
+    # longest-first order starts the class's slowest chunk first and no launch waits behind another's tail
     groups = []
-    for n in np.unique(Nv):
-        i0, i1 = np.searchsorted(Nv, n), np.searchsorted(Nv, n, side="right")
-        groups.append((int(n), int(i0), int(i1), torch.empty((i1 - i0, n + 1, 5), dtype=torch.float64, device=dev),
-                       torch.empty((i1 - i0, n, 2), dtype=torch.float64, device=dev),
-                       torch.empty((i1 - i0, n), dtype=torch.float64, device=dev)))
+    hg = pl.horizon_groups(Nv)
+    for lo_n, hi_n in hg:
+        i0, i1 = np.searchsorted(Nv, lo_n), np.searchsorted(Nv, hi_n, side="right")
+        groups.append((int(hi_n), int(i0), int(i1), torch.empty((i1 - i0, hi_n + 1, 5), dtype=torch.float64, device=dev),
+                       torch.empty((i1 - i0, hi_n, 2), dtype=torch.float64, device=dev),
+                       torch.empty((i1 - i0, hi_n), dtype=torch.float64, device=dev)))
     o = [torch.empty(Bl, dtype=torch.int32, device=dev) for _ in range(3)]
     stream = torch.cuda.current_stream(dev)
-    # the horizon groups run concurrently on side streams (a launch's time is set by its slowest chunk,
-    # so serialised launches would add their tails), the largest horizons first
+    # the launches run concurrently on side streams (a launch's time is set by its slowest chunk, so
+    # serialised launches would add their tails), the largest horizons first
     side = [torch.cuda.Stream(dev) for _ in range(min(4, len(groups)))]
     order = sorted(range(len(groups)), key=lambda g: -groups[g][0])
     d8, d4 = 8, 4
@@ -601,6 +608,7 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
                "status_names": [mpcplan.STATUS_NAMES[i] for i in range(5)],
                "sqp_mean": float(sqp.mean()), "qp_ipm_iters_mean": float(iters.mean()),
                "launches_per_step": len(groups), "streams": len(side),
+               "launch_groups": [{"N": [int(a), int(b)], "chunks_per_cu": pl.chunks_per_cu(b)} for a, b in hg],
                "pipelined": {"value": world * Bl * steps / pel, "unit": "chunks/s", "batches": steps,
                              "note": "the same batches back to back without a join between them (a continuously "
                                      "fed planning service); secondary, value is one batch at a time"},
@@ -609,7 +617,7 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
                                      "recursions, DESIGN.md 5c); executed FP64 from its PMC pass over N = 16, "
                                      "16384 chunks (tools/gpu_plan_pmc.sh)"),
                "note": "HIP events on the timing stream, which joins the side streams that run one launch per "
-                       "horizon; inputs resident in HBM"}
+                       "residency class of horizons; inputs resident in HBM"}
         if with_cpu:
             out["cpu_baseline"], out["parity_sample"] = plan_cpu_baseline(r, wb, cpu_s, status, groups)
             out["cpu_reference"] = plan_cpu_reference(r, wb)
@@ -636,6 +644,7 @@ def plan_fleet(B, device):
     t0 = time.perf_counter()
     plans, summary = TP.optimize_full_trajectory_batch(r, starts, device=device)
     dt = time.perf_counter() - t0
+    tm = TP.optimize_full_trajectory_batch.timing
     t0 = time.perf_counter()
     plans_r, summary_r = TP.optimize_full_trajectory_batch(r, starts, device=device, device_loop=False)
     dt_r = time.perf_counter() - t0
@@ -644,6 +653,11 @@ def plan_fleet(B, device):
     return {"plans": B, "seconds": dt, "plans_per_s": B / dt, "chunks": chunks, "chunks_per_s": chunks / dt,
             "max_chunks_per_plan": max(len(q["statuses"]) for q in summary),
             "checks_passed": int(sum(bool(q["passed"]) for q in summary)),
+            "breakdown": {"launches": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in l.items()}
+                                       for l in tm.get("launches", [])],
+                          "loop_seconds": tm["loop_seconds"], "checks_seconds": tm["seconds"] - tm["loop_seconds"],
+                          "note": "launches: plan_optimize_device calls (launch, run, copy back) per tier (Nmax); "
+                                  "checks: plan assembly and the restated checks on every plan"},
             "round_loop": {"seconds": dt_r, "plans_per_s": B / dt_r, "identical_plans": bool(same),
                            "note": "one batched chunk launch per round from the host (device_loop=False): each "
                                    "round waits for its slowest chunk"},

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCPLAN_VERSION 1
+#define MPCPLAN_VERSION 2
 #define PLAN_MAX_N 64          /* collocation intervals per chunk */
 
 /* status[] codes */
@@ -102,6 +102,14 @@ int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const 
 int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const double* x0,
                              const double* s_target, const int* is_final, double* X, double* U, double* S,
                              int* status, int* iters, int* sqp, void* stream);
+
+/* Chunks resident per compute unit for a plan_solve_chunks_device launch whose LDS is sized for Nmax (the
+ * kernel's registers and Nmax's LDS block; one wavefront per chunk), in *out.  A batch of mixed horizons
+ * solves fastest in as few launches as keep this number: every horizon whose own launch would reach the
+ * same residency goes into one launch sized for the largest of them, with per-chunk N (a launch lasts as
+ * long as its slowest chunk, and the in-launch longest-first order starts that chunk first).  No reference
+ * counterpart: the reference solves one chunk at a time (trajectory_planning.py:491). */
+int plan_chunks_per_cu(plan_ctx* c, int Nmax, int* out);
 
 /* The chunk loop of optimize_full_trajectory (trajectory_planning.py:491-548) for B plans, on the device,
  * asynchronous on `stream`; device pointers.  Replaces the host loop over chunks (:491) for a batch of start

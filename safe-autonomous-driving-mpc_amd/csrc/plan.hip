@@ -248,6 +248,23 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
     return PLAN_SUCCESS;
 }
 
+int plan_chunks_per_cu(plan_ctx* c, int Nmax, int* out) {
+    if (!c || !out) return fail(PLAN_E_ARG, "ctx and out are required");
+    if (Nmax < 1 || Nmax > PLAN_MAX_N) return fail(PLAN_E_ARG, "Nmax out of range [1, PLAN_MAX_N]");
+    const size_t lds = lds_bytes(Nmax);
+    if (lds > c->lds_max) return fail(PLAN_E_ARG, "Nmax too large for the device's LDS");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");
+    if (lds > 65536 &&
+        hipFuncSetAttribute((const void*)plan_chunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(PLAN_E_LAUNCH, "cannot raise the kernel's LDS limit");
+    // one workgroup (one wavefront) per chunk: the residency is set by the kernel's registers and its LDS
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)plan_chunk_kernel, WAVE, lds) != hipSuccess)
+        return fail(PLAN_E_DEVICE, "occupancy query failed");
+    *out = n;
+    return PLAN_SUCCESS;
+}
+
 int plan_optimize_device(plan_ctx* c, int B, int Nmax, const double* starts, double max_chunk_size, int max_chunks,
                          const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final,
                          int* status, int* iters, int* sqp, int* nchunks, void* stream) {

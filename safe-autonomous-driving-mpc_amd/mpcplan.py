@@ -33,7 +33,7 @@ class PlanError(RuntimeError):
 
 
 EXPORTS = ["plan_default_params", "plan_create", "plan_solve_chunks", "plan_solve_chunks_device", "plan_optimize_device",
-           "plan_route_eval", "plan_set_params", "plan_last_error", "plan_version", "plan_destroy"]
+           "plan_route_eval", "plan_chunks_per_cu", "plan_set_params", "plan_last_error", "plan_version", "plan_destroy"]
 
 _lib = None
 
@@ -58,6 +58,8 @@ def lib():
                                         C.c_int] + [C.c_void_p] * 10)
     L.plan_route_eval.restype = C.c_int
     L.plan_route_eval.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]
+    L.plan_chunks_per_cu.restype = C.c_int
+    L.plan_chunks_per_cu.argtypes = [C.c_void_p, C.c_int, _ip]
     L.plan_set_params.restype = C.c_int
     L.plan_set_params.argtypes = [C.c_void_p, C.POINTER(PlanParams)]
     L.plan_last_error.restype = C.c_char_p
@@ -148,6 +150,25 @@ class Planner:
                                               X_ptr or None, U_ptr or None, S_ptr or None, status_ptr or None,
                                               iters_ptr or None, sqp_ptr or None, C.c_void_p(stream)),
                "plan_solve_chunks_device")
+
+    def chunks_per_cu(self, Nmax):
+        """plan_chunks_per_cu: chunks resident per compute unit for a launch sized for Nmax."""
+        n = C.c_int(0)
+        _check(lib().plan_chunks_per_cu(self.h, int(Nmax), C.byref(n)), "plan_chunks_per_cu")
+        return n.value
+
+    def horizon_groups(self, horizons):
+        """Launch groups for a batch of mixed horizons: runs of consecutive distinct horizons (ascending) whose
+        launch sized for the run's largest horizon keeps the residency each would reach alone
+        (include/mpcplan.h, plan_chunks_per_cu).  Returns [(N_lo, N_hi), ...]."""
+        hs = sorted({int(n) for n in np.asarray(horizons).ravel()})
+        groups = []
+        for n in hs:
+            if groups and self.chunks_per_cu(n) == self.chunks_per_cu(groups[-1][0]):
+                groups[-1] = (groups[-1][0], n)
+            else:
+                groups.append((n, n))
+        return groups
 
     def optimize_device(self, starts, max_chunk_size, max_chunks, avg, Nmax, device=0):
         """plan_optimize_device (include/mpcplan.h): the chunk loop of optimize_full_trajectory for B plans on

@@ -12,6 +12,7 @@ loop (:419-559) and ends with reference_trajectory_check (:557).  Route acquisit
 GraphHopper over HTTP) is out of scope: routes.py builds the route from local way-points.
 """
 import math
+import time
 
 import numpy as np
 
@@ -263,9 +264,16 @@ def _commit(pieces, X, U, S, n, fin):
     return pieces[-1][0][-1]
 
 
-def _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, statuses, horizons, opt, seg=64):
+def _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, statuses, horizons, opt, seg=64,
+                 timing=None):
     """optimize_full_trajectory_batch's chunk loop as plan_optimize_device launches: every plan advances on its
-    own wavefront, up to `seg` chunks per launch (plans still running continue from their last start)."""
+    own wavefront, up to `seg` chunks per launch (plans still running continue from their last start).
+
+    Two tiers when that raises the residency (mpcplan.Planner.chunks_per_cu): the launches are first sized for
+    the longest intermediate chunk's horizon (size max_chunk_size), which holds every chunk but the longer
+    final ones; a plan whose next chunk does not fit there stops (nchunks = -(n + 1), its first n chunks
+    solved) and continues in launches sized for the longest final chunk (size < 2 max_chunk_size).  A chunk's
+    result does not depend on the launch's LDS sizing, so the plans are the same bit for bit."""
     s_total = route.s_total
     vm = np.asarray(route.vmax, np.float64)
     avg = np.array([float(np.mean(vm[i:])) for i in range(vm.size)])     # route.avg_speed_from(5 i), :507
@@ -274,27 +282,44 @@ def _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, stat
     opt.N, opt.dt = Nmax, 0.3
     pl = mpcplan.Planner(route, opt.params(0.0), device=device)
     try:
+        n_mid = min(max(int(np.max(np.ceil(max_chunk_size / avg * 2.0 / 0.3))), 1), Nmax)
+        tiers = [n_mid, Nmax] if pl.chunks_per_cu(n_mid) > pl.chunks_per_cu(Nmax) else [Nmax]
         cur = np.asarray(starts, np.float64).copy()
         act = np.arange(cur.shape[0])
-        used = 0
-        while act.size and used < max_chunks:
-            C_ = min(seg, max_chunks - used)
-            r = pl.optimize_device(cur[act], max_chunk_size, C_, avg, Nmax, device=device)
-            nxt = []
-            for i, b in enumerate(act):
-                nc = int(r["nchunks"][i])
-                for j in range(abs(nc) - (1 if nc < 0 else 0)):
-                    n, fin = int(r["N"][i, j]), int(r["is_final"][i, j])
-                    statuses[b].append(int(r["status"][i, j]))
-                    horizons[b].append(n)
-                    cur[b] = _commit(pieces[b], r["X"][i, j, :n + 1], r["U"][i, j, :n], r["S"][i, j, :n], n, fin)
-                if nc < 0:
-                    raise ValueError(f"chunk horizon of plan {b} exceeds PLAN_MAX_N={mpcplan.PLAN_MAX_N} (or its "
-                                     f"start lies past the end of the route)")
-                if nc == C_ and s_total - cur[b, 0] > 0.1:
-                    nxt.append(b)
-            used += C_
-            act = np.array(nxt, dtype=int)
+        used = np.zeros(cur.shape[0], int)
+        for t, Nm in enumerate(tiers):
+            last = t == len(tiers) - 1
+            later = []
+            while act.size:
+                C_ = int(min(seg, max_chunks - used[act].min()))
+                if C_ <= 0:
+                    break
+                t0 = time.perf_counter()
+                r = pl.optimize_device(cur[act], max_chunk_size, C_, avg, Nm, device=device)
+                if timing is not None:
+                    timing.setdefault("launches", []).append({"Nmax": int(Nm), "plans": int(act.size), "slots": C_,
+                                                              "seconds": time.perf_counter() - t0})
+                nxt = []
+                for i, b in enumerate(act):
+                    nc = int(r["nchunks"][i])
+                    nc_ok = abs(nc) - (1 if nc < 0 else 0)
+                    for j in range(min(nc_ok, max_chunks - used[b])):
+                        n, fin = int(r["N"][i, j]), int(r["is_final"][i, j])
+                        statuses[b].append(int(r["status"][i, j]))
+                        horizons[b].append(n)
+                        cur[b] = _commit(pieces[b], r["X"][i, j, :n + 1], r["U"][i, j, :n], r["S"][i, j, :n], n, fin)
+                        used[b] += 1
+                    if used[b] >= max_chunks or s_total - cur[b, 0] <= 0.1:
+                        continue
+                    if nc < 0:
+                        if last:
+                            raise ValueError(f"chunk horizon of plan {b} exceeds PLAN_MAX_N={mpcplan.PLAN_MAX_N} (or "
+                                             f"its start lies past the end of the route)")
+                        later.append(b)             # its next chunk needs the larger tier's LDS
+                    elif nc == C_:
+                        nxt.append(b)
+                act = np.array(nxt, dtype=int)
+            act = np.array(sorted(later), dtype=int)
     finally:
         pl.close()
 
@@ -317,6 +342,8 @@ def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=
     if isinstance(route, dict):
         import routes
         route = routes.from_graphhopper(route)
+    t_start = time.perf_counter()
+    timing = {}
     starts = np.atleast_2d(np.asarray(starts, np.float64))
     B = starts.shape[0]
     s_total = route.s_total
@@ -328,7 +355,8 @@ def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=
     opt = TrajectoryOptimizer(device=device)
     pl = None
     if solve_chunks is None and device_loop:
-        _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, statuses, horizons, opt)
+        _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, statuses, horizons, opt,
+                     timing=timing)
         max_chunks = 0                                                 # the host loop below does not run
     for _ in range(max_chunks):
         act = np.flatnonzero(~done & (s_total - cur[:, 0] > 0.1))
@@ -358,6 +386,7 @@ def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=
             cur[b] = _commit(pieces[b], X, U, S, n, fin[i])
     if pl is not None:
         pl.close()
+    timing["loop_seconds"] = time.perf_counter() - t_start
     plans, summary = [], []
     for b in range(B):
         if not pieces[b]:
@@ -371,4 +400,6 @@ def optimize_full_trajectory_batch(route, starts, max_chunk_size=20, max_chunks=
         q = plan_check_summary(opt.u_min, opt.u_max, X, U, S, s_total)
         q["statuses"], q["horizons"] = statuses[b], horizons[b]
         summary.append(q)
+    timing["seconds"] = time.perf_counter() - t_start
+    optimize_full_trajectory_batch.timing = timing
     return plans, summary

@@ -284,3 +284,34 @@ def test_longest_first_order_changes_nothing(env, monkeypatch):
           f"{np.bincount(oa[0].cpu().numpy(), minlength=5).tolist()}")
     plain.close()
     ordered.close()
+
+
+def test_residency_groups(env):
+    """plan_chunks_per_cu is non-increasing in Nmax and at least 1 up to PLAN_MAX_N; Planner.horizon_groups
+    puts each horizon in one launch whose residency equals its own launch's; the grouped launches (per-chunk N,
+    LDS sized for the group's largest horizon) give each chunk's plan bit for bit as one launch per horizon."""
+    mpcplan, PO, W = env
+    r = W.plan_route("traj3")
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=16))
+    occ = [pl.chunks_per_cu(n) for n in range(1, mpcplan.PLAN_MAX_N + 1)]
+    assert min(occ) >= 1 and all(a >= b for a, b in zip(occ, occ[1:])), occ
+    hs = [13, 14, 16, 17, 25, 28, 32]
+    groups = pl.horizon_groups(hs)
+    assert sorted(n for n in hs if any(lo <= n <= hi for lo, hi in groups)) == hs
+    for lo, hi in groups:
+        for n in hs:
+            if lo <= n <= hi:
+                assert pl.chunks_per_cu(n) == pl.chunks_per_cu(hi)
+    parts = {n: W.plan_batch(r, n, 24, seed=30 + n, final_frac=0.2) for n in hs}
+    for lo, hi in groups:
+        mem = [n for n in hs if lo <= n <= hi]
+        x0 = np.concatenate([parts[n]["x0"] for n in mem]); st = np.concatenate([parts[n]["s_target"] for n in mem])
+        fin = np.concatenate([parts[n]["is_final"] for n in mem]); N = np.repeat(mem, 24).astype(np.int32)
+        g = pl.solve_chunks(x0, st, fin, N)
+        for i, n in enumerate(mem):
+            pl.set_params(mpcplan.default_params(N=n))
+            one = pl.solve_chunks(parts[n]["x0"], parts[n]["s_target"], parts[n]["is_final"])
+            sl = slice(24 * i, 24 * i + 24)
+            assert np.array_equal(one["X"], g["X"][sl, :n + 1]) and np.array_equal(one["status"], g["status"][sl])
+    print(f"\nchunks per CU by Nmax: {dict(zip(range(1, 65), occ))}; groups of {hs}: {groups}")
+    pl.close()

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(built):
     out = subprocess.run(["nm", "-D", "--defined-only", built], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"\sT\s+(plan_[a-z_]+)$", out, flags=re.M))
     names = declared_functions()
-    assert len(names) == 10 and not [n for n in names if n not in exported]
+    assert len(names) == 11 and not [n for n in names if n not in exported]
     import mpcplan
     assert sorted(mpcplan.EXPORTS) == names
 
@@ -99,3 +99,17 @@ def test_drop_in_surface():
     assert abs(t.cost(z, x, r.s_total) - ch.cost(z)) <= 1e-12 * abs(ch.cost(z))
     with pytest.raises(TypeError, match="routes.Route"):
         t.optimize(x, 30.0, r.s_total, lambda s: 0.0, lambda s: 0, lambda s: 13.0, False)
+
+
+def test_horizon_groups_follow_the_residency(built):
+    """Planner.horizon_groups (host logic; residency stubbed, plan_chunks_per_cu needs a GPU): consecutive
+    horizons share a launch while the launch sized for the largest keeps each one's residency."""
+    import mpcplan
+    pl = object.__new__(mpcplan.Planner)
+    occ = lambda n: 4 if n <= 17 else (3 if n <= 23 else 2)
+    pl.chunks_per_cu = occ
+    assert pl.horizon_groups([13, 14, 17, 16, 25, 32, 13]) == [(13, 17), (25, 32)]
+    assert pl.horizon_groups(np.array([20, 18, 24, 30])) == [(18, 20), (24, 30)]
+    assert pl.horizon_groups([5]) == [(5, 5)]
+    assert pl.horizon_groups([]) == []
+    pl.h = None

@@ -69,6 +69,7 @@ static inline double dpp_row_bcast(double v, int L) {
     pthread_barrier_wait(&g_bar);
     return r;
 }
+static inline int atomicAdd(int* p, int v) { return __atomic_fetch_add(p, v, __ATOMIC_SEQ_CST); }
 #define PLAN_HOST_EMU 1
 
 #include "../safe-autonomous-driving-mpc_amd/csrc/plan_kernel.h"

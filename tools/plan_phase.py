@@ -1,7 +1,9 @@
 """Planner phase profile: runs B chunks through the diagnostic build libmpcplan_prof.so (-DPLAN_PROF) and
 prints the wave time per kernel phase (s_memtime ticks summed over chunks; each phase inclusive of the phases
 nested in it: factor and solve run inside ipm_rows / eqp_rows, rollout inside both), as a share of the total.
-usage: python tools/plan_phase.py N B1,B2,... [route] [final_frac]"""
+usage: python tools/plan_phase.py N B1,B2,... [route] [final_frac]
+       python tools/plan_phase.py bench <route> <B> i1,i2,...   (bench.py's plan-leg chunks i1, i2, ... of a
+                                                                 B-chunk mix, seed 7, each alone)"""
 import ctypes as C
 import os
 import sys
@@ -19,26 +21,21 @@ import workloads as W
 PHASES = ["TOTAL", "build_qp", "stage_hess", "factor", "solve", "ipm_rows", "eqp_rows", "multipliers",
           "line_search", "rollout"]
 
-N = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-Bs = sys.argv[2] if len(sys.argv) > 2 else "64,4096"
-route = sys.argv[3] if len(sys.argv) > 3 else "traj1"
-ff = float(sys.argv[4]) if len(sys.argv) > 4 else 0.25
 L = mpcplan.lib()
 L.plan_debug_prof.restype = C.c_int
 L.plan_debug_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-r = W.plan_route(route)
-for B in [int(x) for x in Bs.split(",")]:
-    wb = W.plan_batch(r, N, B, seed=N, final_frac=ff)
-    pl = mpcplan.Planner(r, mpcplan.default_params(N=N))
+
+
+def profile(pl, label, N, x0, st, fin):
     buf = (C.c_ulonglong * 16)()
-    print(f"B={B}: reset rc {L.plan_debug_prof(buf, 1)}", flush=True)
+    L.plan_debug_prof(buf, 1)
     t0 = time.perf_counter()
-    g = pl.solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    g = pl.solve_chunks(x0, st, fin)
     wall = time.perf_counter() - t0
     L.plan_debug_prof(buf, 0)
     v = np.array(buf[:len(PHASES)], dtype=np.float64)
     tot = v[0]
-    print(f"N={N} B={B} {route}: wall {wall * 1e3:.1f} ms, chunks counted {buf[15]}, sqp mean {g['sqp'].mean():.2f}, "
+    print(f"{label}: wall {wall * 1e3:.1f} ms, chunks counted {buf[15]}, sqp mean {g['sqp'].mean():.2f}, "
           f"ipm iters mean {g['iters'].mean():.1f}, status {np.bincount(g['status'], minlength=5).tolist()}")
     print(f"ticks per chunk {tot / max(1, buf[15]):.3e}")
     for n, x in zip(PHASES, v):
@@ -49,4 +46,29 @@ for B in [int(x) for x in Bs.split(",")]:
         # two terminal-response solves inside a factorisation)
         print(f"  factorisations {nf}: {v[3] / nf:.0f} cycles each = {v[3] / nf / N:.0f} per stage; solves {ns}: "
               f"{v[4] / ns:.0f} cycles each = {v[4] / ns / N:.0f} per stage", flush=True)
+        it = float(g["iters"].sum())
+        if it:
+            print(f"  per interior-point iteration (all phases): {tot / it:.0f} cycles", flush=True)
+
+
+if sys.argv[1] == "bench":
+    route, B, idx = sys.argv[2], int(sys.argv[3]), [int(x) for x in sys.argv[4].split(",")]
+    r = W.plan_route(route)
+    wb = W.plan_batch_ref(r, B, seed=7)
+    for i in idx:
+        n = int(wb["N"][i])
+        pl = mpcplan.Planner(r, mpcplan.default_params(N=n))
+        profile(pl, f"{route} bench chunk {i} N={n}", n, wb["x0"][i:i + 1], wb["s_target"][i:i + 1],
+                wb["is_final"][i:i + 1])
+        pl.close()
+    sys.exit(0)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+Bs = sys.argv[2] if len(sys.argv) > 2 else "64,4096"
+route = sys.argv[3] if len(sys.argv) > 3 else "traj1"
+ff = float(sys.argv[4]) if len(sys.argv) > 4 else 0.25
+r = W.plan_route(route)
+for B in [int(x) for x in Bs.split(",")]:
+    wb = W.plan_batch(r, N, B, seed=N, final_frac=ff)
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=N))
+    profile(pl, f"N={N} B={B} {route}", N, wb["x0"], wb["s_target"], wb["is_final"])
     pl.close()

@@ -48,4 +48,7 @@ for B in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4096,16384,655
     print(f"N={N} B={B} route={route}: {np.mean(ms):.2f} ms/launch = {B / np.mean(ms) * 1e3:.0f} chunks/s; "
           f"sqp mean {sq.mean():.2f} max {sq.max()}, ipm mean {it.mean():.1f} max {it.max()}, "
           f"status {np.bincount(stt, minlength=5).tolist()} (gen {tg:.1f}s)", flush=True)
+    if os.environ.get("PLAN_DUMP"):     # results for a bit-for-bit A/B of library variants
+        np.savez(os.path.join(ROOT, "gpurun_out", f"plan_dump_{os.environ.get('PLAN_LIB', 'libmpcplan.so')}_{N}_{B}.npz"),
+                 X=X.cpu().numpy(), U=U.cpu().numpy(), S=S.cpu().numpy(), status=stt, iters=it, sqp=sq)
     pl.close()
