@@ -386,16 +386,20 @@ __device__ inline RowSp row_sp(int kind, bool has_w, double kb, double vb) {
         default: return {0, 0, 1.0, 0.0, false};        // ROW_STERM
     }
 }
-// f(kind, j) for the rows of stage k in storage order (j = the row's slot)
+// f(kind, j, on) for every row kind of stage k, in storage order: j = the row's slot when on (the stage has
+// the row), else a valid slot of the stage (clamped) whose values the body must not use.  The body runs
+// unconditionally -- loads, divisions and all -- and applies its results under `on` (selects, masked stores):
+// no branch per kind, so the scheduler overlaps the rows' independent chains (one lane serves a stage, so
+// the rows are its serial work); every on-row value is computed by the same operations as before.
 template <class F>
 __device__ inline void for_rows(int k, int N, int fin, F&& f) {
     int j = 0;
 #pragma unroll
-    for (int kind = 0; kind <= ROW_STERM; ++kind)
-        if (row_on(kind, k, N, fin)) {
-            f(kind, j);
-            ++j;
-        }
+    for (int kind = 0; kind <= ROW_STERM; ++kind) {
+        const bool on = row_on(kind, k, N, fin);
+        f(kind, j < NR ? j : NR - 1, on);
+        j += on ? 1 : 0;
+    }
 }
 // g + a . z
 __device__ inline double sp_dot(const RowSp& r, double g, const double z[NZ]) {
@@ -819,14 +823,18 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
             if (i < nv) H[hx(i, i)] += X.delta;
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         const unsigned act = mode == 0 ? 0u : (unsigned)L[Y.oTACT + k];
-        for_rows(k, N, X.fin, [&](int kind, int j) {
+        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
             const double w = mode == 0 ? L[Y.oLAM + NR * k + j] / L[Y.oS + NR * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
-            if (w == 0.0) return;
+            const bool use = on && w != 0.0;
             const RowSp r = row_sp(kind, k < N, kb, vb);
-            H[hx(r.i0, r.i0)] += w * r.c0 * r.c0;
+            const int a = hx(r.i0, r.i0), b = hx(r.i0, r.i1), c = hx(r.i1, r.i1);
+            const double ha = H[a] + w * r.c0 * r.c0;
+            H[a] = use ? ha : H[a];
             if (r.two) {
-                H[hx(r.i0, r.i1)] += w * r.c0 * r.c1;
-                H[hx(r.i1, r.i1)] += w * r.c1 * r.c1;
+                const double hb = H[b] + w * r.c0 * r.c1;
+                H[b] = use ? hb : H[b];
+                const double hc = H[c] + w * r.c1 * r.c1;
+                H[c] = use ? hc : H[c];
             }
         });
         ldsd* hs = L + Y.oHS + 8 * k;
@@ -1289,12 +1297,16 @@ __device__ int eqp(Ctx& X, double scale) {
             for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
             const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
             const unsigned act = (unsigned)L[Y.oTACT + k];
-            for_rows(k, N, X.fin, [&](int kind, int j) {
-                if (!((act >> j) & 1u)) return;
+            for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+                const bool use = on && ((act >> j) & 1u);
                 const RowSp r = row_sp(kind, k < N, kb, vb);
                 const double f = RHO * sp_dot(r, L[Y.oG + NR * k + j], z) - L[Y.oY + NR * k + j];
-                g[r.i0] += f * r.c0;
-                if (r.two) g[r.i1] += f * r.c1;
+                const double g0 = g[r.i0] + f * r.c0;
+                g[r.i0] = use ? g0 : g[r.i0];
+                if (r.two) {
+                    const double g1 = g[r.i1] + f * r.c1;
+                    g[r.i1] = use ? g1 : g[r.i1];
+                }
             });
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
@@ -1311,14 +1323,13 @@ __device__ int eqp(Ctx& X, double scale) {
             for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
             const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
             const unsigned act = (unsigned)L[Y.oTACT + k];
-            for_rows(k, N, X.fin, [&](int kind, int j) {
-                if ((act >> j) & 1u) {
-                    const double d = RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
-                    const double y = L[Y.oY + NR * k + j] - d;
-                    L[Y.oY + NR * k + j] = y;
-                    upd = fmax(upd, fabs(d));
-                    ym = fmax(ym, fabs(y));
-                }
+            for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+                const bool use = on && ((act >> j) & 1u);
+                const double d = RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
+                const double y = L[Y.oY + NR * k + j] - d;
+                if (use) L[Y.oY + NR * k + j] = y;
+                upd = use ? fmax(upd, fabs(d)) : upd;
+                ym = use ? fmax(ym, fabs(y)) : ym;
             });
         }
         upd = wmax(upd);
@@ -1338,16 +1349,14 @@ __device__ int eqp(Ctx& X, double scale) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-        for_rows(k, N, X.fin, [&](int kind, int j) {
+        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
             const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
-            if ((mask >> j) & 1u) {
-                const double y = L[Y.oY + NR * k + j];
-                L[Y.oTLAM + NR * k + j] = y;
-                if (y < -tl || fabs(rv) > tr) { mask &= ~(1u << j); ++bad; }
-            } else {
-                L[Y.oTLAM + NR * k + j] = 0.0;
-                if (rv < -tr) { mask |= 1u << j; ++bad; }
-            }
+            const double y = L[Y.oY + NR * k + j];
+            const bool in = (mask >> j) & 1u;
+            if (on) L[Y.oTLAM + NR * k + j] = in ? y : 0.0;
+            const bool flip = on && (in ? (y < -tl || fabs(rv) > tr) : rv < -tr);
+            mask = flip ? (mask ^ (1u << j)) : mask;
+            bad += flip ? 1 : 0;
         });
         L[Y.oTACT + k] = (double)mask;
     }
@@ -1373,13 +1382,15 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-        for_rows(k, N, X.fin, [&](int kind, int j) {
+        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
             if (!resume) {
                 const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
-                L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
-                L[Y.oLAM + NR * k + j] = 1.0;
+                if (on) {
+                    L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
+                    L[Y.oLAM + NR * k + j] = 1.0;
+                }
             }
-            ++m;
+            m += on ? 1 : 0;
         });
     }
     m = wsumi(m);
@@ -1390,7 +1401,11 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         double mu = 0.0;
         for (int k = X.ln; k <= N; k += WAVE) {
             const int nr = stage_nrows(k, N, X.fin);
-            for (int j = 0; j < nr; ++j) mu += L[Y.oS + NR * k + j] * L[Y.oLAM + NR * k + j];
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {      // every slot, the stage's rows applied (see for_rows)
+                const double t = mu + L[Y.oS + NR * k + j] * L[Y.oLAM + NR * k + j];
+                mu = j < nr ? t : mu;
+            }
         }
         mu = wsum(mu) / m;
         if (!isfinite(mu)) { rc = -1; break; }
@@ -1399,9 +1414,10 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             double tie = 0.0;
             for (int k = X.ln; k <= N; k += WAVE) {
                 const int nr = stage_nrows(k, N, X.fin);
-                for (int j = 0; j < nr; ++j) {
+#pragma unroll
+                for (int j = 0; j < NR; ++j) {
                     const double sv = L[Y.oS + NR * k + j], lv = L[Y.oLAM + NR * k + j];
-                    if (!(sv > CHECK_SEP * lv || lv > CHECK_SEP * sv)) tie = 1.0;
+                    if (j < nr && !(sv > CHECK_SEP * lv || lv > CHECK_SEP * sv)) tie = 1.0;
                 }
             }
             if (wmax(tie) == 0.0) { rc = 2; break; }
@@ -1415,19 +1431,24 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 double am = 1.0;
                 for (int k = X.ln; k <= N; k += WAVE) {
                     const int nr = stage_nrows(k, N, X.fin);
-                    for (int j = 0; j < nr; ++j) {
+#pragma unroll
+                    for (int j = 0; j < NR; ++j) {
                         const double dsa = L[Y.oDSA + NR * k + j], dla = L[Y.oDLA + NR * k + j];
-                        if (dsa < 0.0) am = fmin(am, -L[Y.oS + NR * k + j] / dsa);
-                        if (dla < 0.0) am = fmin(am, -L[Y.oLAM + NR * k + j] / dla);
+                        const double rs = -L[Y.oS + NR * k + j] / dsa, rl = -L[Y.oLAM + NR * k + j] / dla;
+                        am = (j < nr && dsa < 0.0) ? fmin(am, rs) : am;
+                        am = (j < nr && dla < 0.0) ? fmin(am, rl) : am;
                     }
                 }
                 am = wmin(am);
                 double mua = 0.0;
                 for (int k = X.ln; k <= N; k += WAVE) {
                     const int nr = stage_nrows(k, N, X.fin);
-                    for (int j = 0; j < nr; ++j)
-                        mua += (L[Y.oS + NR * k + j] + am * L[Y.oDSA + NR * k + j]) *
-                               (L[Y.oLAM + NR * k + j] + am * L[Y.oDLA + NR * k + j]);
+#pragma unroll
+                    for (int j = 0; j < NR; ++j) {
+                        const double t = mua + (L[Y.oS + NR * k + j] + am * L[Y.oDSA + NR * k + j]) *
+                                                   (L[Y.oLAM + NR * k + j] + am * L[Y.oDLA + NR * k + j]);
+                        mua = j < nr ? t : mua;
+                    }
                 }
                 mua = wsum(mua) / m;
                 const double ratio = mua / mu;
@@ -1440,15 +1461,19 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
 #pragma unroll
                 for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
                 const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-                for_rows(k, N, X.fin, [&](int kind, int j) {
+                for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
                     const RowSp r = row_sp(kind, k < N, kb, vb);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
                     double rs = -s * l;
                     if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
                     const double rp = sp_dot(r, L[Y.oG + NR * k + j], z) - s;
                     const double f = l + (rs - l * rp) / s;
-                    g[r.i0] -= f * r.c0;
-                    if (r.two) g[r.i1] -= f * r.c1;
+                    const double g0 = g[r.i0] - f * r.c0;
+                    g[r.i0] = on ? g0 : g[r.i0];
+                    if (r.two) {
+                        const double g1 = g[r.i1] - f * r.c1;
+                        g[r.i1] = on ? g1 : g[r.i1];
+                    }
                 });
 #pragma unroll
                 for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
@@ -1466,7 +1491,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                     dz[u] = L[Y.oDZ + ZS * k + u];
                 }
                 const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-                for_rows(k, N, X.fin, [&](int kind, int j) {
+                for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
                     const RowSp r = row_sp(kind, k < N, kb, vb);
                     const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
                     double rs = -s * l;
@@ -1474,8 +1499,11 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                     double v = sp_dot(r, L[Y.oG + NR * k + j], z) - s;
                     v += r.c0 * dz[r.i0];
                     if (r.two) v += r.c1 * dz[r.i1];
-                    L[ods + NR * k + j] = v;
-                    L[odl + NR * k + j] = (rs - l * v) / s;
+                    const double dl = (rs - l * v) / s;
+                    if (on) {
+                        L[ods + NR * k + j] = v;
+                        L[odl + NR * k + j] = dl;
+                    }
                 });
             }
             sync();
@@ -1483,10 +1511,12 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         double amax = 1.0 / TAU, fin = 1.0;
         for (int k = X.ln; k <= N; k += WAVE) {
             const int nr = stage_nrows(k, N, X.fin);
-            for (int j = 0; j < nr; ++j) {
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
                 const double ds = L[Y.oDS + NR * k + j], dl = L[Y.oDL + NR * k + j];
-                if (ds < 0.0) amax = fmin(amax, -L[Y.oS + NR * k + j] / ds);
-                if (dl < 0.0) amax = fmin(amax, -L[Y.oLAM + NR * k + j] / dl);
+                const double rs = -L[Y.oS + NR * k + j] / ds, rl = -L[Y.oLAM + NR * k + j] / dl;
+                amax = (j < nr && ds < 0.0) ? fmin(amax, rs) : amax;
+                amax = (j < nr && dl < 0.0) ? fmin(amax, rl) : amax;
             }
 #pragma unroll
             for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oDZ + ZS * k + u]) ? fin : 0.0;
@@ -1499,9 +1529,14 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oZ + ZS * k + u] += alpha * L[Y.oDZ + ZS * k + u];
             const int nr = stage_nrows(k, N, X.fin);
-            for (int j = 0; j < nr; ++j) {
-                L[Y.oS + NR * k + j] += alpha * L[Y.oDS + NR * k + j];
-                L[Y.oLAM + NR * k + j] += alpha * L[Y.oDL + NR * k + j];
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const double sn = L[Y.oS + NR * k + j] + alpha * L[Y.oDS + NR * k + j];
+                const double ln_ = L[Y.oLAM + NR * k + j] + alpha * L[Y.oDL + NR * k + j];
+                if (j < nr) {
+                    L[Y.oS + NR * k + j] = sn;
+                    L[Y.oLAM + NR * k + j] = ln_;
+                }
             }
         }
         sync();
@@ -1531,8 +1566,9 @@ __device__ void accept_polish(const Ctx& X, bool with_act) {
 __device__ double ipm_mask(const Ctx& X, int k) {
     const int nr = stage_nrows(k, X.N, X.fin);
     unsigned m = 0;
-    for (int j = 0; j < nr; ++j)
-        if (X.L[X.Y.oS + NR * k + j] < X.L[X.Y.oLAM + NR * k + j]) m |= 1u << j;
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+        if (j < nr && X.L[X.Y.oS + NR * k + j] < X.L[X.Y.oLAM + NR * k + j]) m |= 1u << j;
     return (double)m;
 }
 
@@ -1544,7 +1580,8 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
     double scale = 1.0;
     for (int k = X.ln; k <= N; k += WAVE) {
         const int nr = stage_nrows(k, N, X.fin);
-        for (int j = 0; j < nr; ++j) scale = fmax(scale, fabs(L[Y.oG + NR * k + j]));
+#pragma unroll
+        for (int j = 0; j < NR; ++j) scale = j < nr ? fmax(scale, fabs(L[Y.oG + NR * k + j])) : scale;
     }
     scale = wmax(scale);
     *iters = 0;
@@ -1621,13 +1658,17 @@ __device__ void multipliers(Ctx& X) {
         L[Y.oMLAT + 2 * k] = 0.0;
         L[Y.oMLAT + 2 * k + 1] = 0.0;
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-        for_rows(k, N, X.fin, [&](int kind, int j) {
+        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
             const RowSp r = row_sp(kind, k < N, kb, vb);
             const double l = L[Y.oLAM + NR * k + j];
-            g[r.i0] -= l * r.c0;
-            if (r.two) g[r.i1] -= l * r.c1;
-            if (kind == ROW_LATP) L[Y.oMLAT + 2 * k] = l;
-            if (kind == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
+            const double g0 = g[r.i0] - l * r.c0;
+            g[r.i0] = on ? g0 : g[r.i0];
+            if (r.two) {
+                const double g1 = g[r.i1] - l * r.c1;
+                g[r.i1] = on ? g1 : g[r.i1];
+            }
+            if (on && kind == ROW_LATP) L[Y.oMLAT + 2 * k] = l;
+            if (on && kind == ROW_LATM) L[Y.oMLAT + 2 * k + 1] = l;
         });
 #pragma unroll
         for (int u = 0; u < 5; ++u) L[Y.oGL + ZS * k + u] = g[u];
@@ -1699,29 +1740,21 @@ __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
             for (int i = 0; i < 5; ++i) v += fabs(def[i]);
         }
         const double kk = x[3], vv = x[4];
-        double g[12];
-        int n = 0;
-        if (!(X.fin && k == N)) {
-            g[n++] = vv + sl - P.v_min;
-            g[n++] = L[Y.oVL + k] - (vv + sl);
-            if (k > 0) {
-                g[n++] = P.a_max - kk * vv * vv;
-                g[n++] = P.a_max + kk * vv * vv;
-            }
-        }
-        if (k > 0) {
-            g[n++] = kk - P.k_min;
-            g[n++] = P.k_max - kk;
-        }
-        if (k < N) {
-            g[n++] = u1 - P.u_min[0];
-            g[n++] = P.u_max[0] - u1;
-            g[n++] = u2 - P.u_min[1];
-            g[n++] = P.u_max[1] - u2;
-            g[n++] = sl;
-        }
-        if (k == N && !X.fin) g[n++] = x[0] - X.st / 2.0;
-        for (int j = 0; j < n; ++j) v += g[j] < 0.0 ? -g[j] : 0.0;
+        // the rows' violations in storage order (a per-lane array indexed at run time would live in scratch)
+        auto add = [&](bool on, double g) { v = on ? v + (g < 0.0 ? -g : 0.0) : v; };
+        const bool sp = !(X.fin && k == N);
+        add(sp, vv + sl - P.v_min);
+        add(sp, L[Y.oVL + k] - (vv + sl));
+        add(sp && k > 0, P.a_max - kk * vv * vv);
+        add(sp && k > 0, P.a_max + kk * vv * vv);
+        add(k > 0, kk - P.k_min);
+        add(k > 0, P.k_max - kk);
+        add(k < N, u1 - P.u_min[0]);
+        add(k < N, P.u_max[0] - u1);
+        add(k < N, u2 - P.u_min[1]);
+        add(k < N, P.u_max[1] - u2);
+        add(k < N, sl);
+        add(k == N && !X.fin, x[0] - X.st / 2.0);
         if (k == N && X.fin) v += fabs(x[0] - X.st) + fabs(x[4]);
     }
     *f = wsum(c);
@@ -1800,7 +1833,8 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
 #pragma unroll
                 for (int i = 0; i < 5; ++i) mu_l = fmax(mu_l, 2.0 * fabs(L[Y.oMY + 5 * k + i]));
             const int nr = stage_nrows(k, N, X.fin);
-            for (int j = 0; j < nr; ++j) mu_l = fmax(mu_l, 2.0 * fabs(L[Y.oLAM + NR * k + j]));
+#pragma unroll
+            for (int j = 0; j < NR; ++j) mu_l = j < nr ? fmax(mu_l, 2.0 * fabs(L[Y.oLAM + NR * k + j])) : mu_l;
         }
         full = wmax(full);
         mu_m = fmax(mu_m, wmax(mu_l));
