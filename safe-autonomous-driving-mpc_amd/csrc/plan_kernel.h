@@ -1005,8 +1005,40 @@ __device__ inline void sol_w(double w[3], double x, const double K[15]) {
 
 // LQ solve over the wave with zero initial state and homogeneous dynamics: stage linear terms at ogl -> odz
 // (the caller syncs before reading odz).  Backward: p_{k} = gx_k + A_k' p_{k+1} + K_k' h_k with h = gw + B' p
-// (lane i: p_i), kk_k = -(L D L')^-1 h_k stored by lane 0; forward: w = kk + K x, x <- A x + B w (lane i: x_i).
-// oracle solve_core().
+// (lane i: p_i); the control right-hand sides h_k go to odz's w slots, and after the recursion every stage
+// forms its feed-forward kk_k = -(L D L')^-1 h_k at once (lane k); forward: w = kk + K x, x <- A x + B w
+// (lane i: x_i).  Each recursion loads stage k - 1's (k + 1's) data while it works on stage k, so a stage
+// waits on no LDS read: what remains on its chain are the broadcast FMAs.  oracle solve_core().
+struct SolBk { double B0[5], B1[5], Ac[5], Kc[3], h0, h1, h2, gx; };
+struct SolFw { double K[15], Ar[5], b0, b1, t[3]; };
+__device__ inline void sol_load_bk(const Ctx& X, int ogl, int k, int me, SolBk& R) {
+    const ldsd* L = X.L;
+    const Layout& Y = X.Y;
+#pragma unroll
+    for (int l = 0; l < 5; ++l) {
+        R.B0[l] = L[Y.oB + 10 * k + 2 * l];
+        R.B1[l] = L[Y.oB + 10 * k + 2 * l + 1];
+        R.Ac[l] = L[Y.oA + 25 * k + 5 * l + me];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r) R.Kc[r] = L[Y.oK + 15 * k + 5 * r + me];
+    R.h0 = L[ogl + ZS * k + 5];
+    R.h1 = L[ogl + ZS * k + 6];
+    R.h2 = L[ogl + ZS * k + 7];
+    R.gx = L[ogl + ZS * k + me];
+}
+__device__ inline void sol_load_fw(const Ctx& X, int odz, int k, int me, SolFw& R) {
+    const ldsd* L = X.L;
+    const Layout& Y = X.Y;
+#pragma unroll
+    for (int i = 0; i < 15; ++i) R.K[i] = L[Y.oK + 15 * k + i];
+#pragma unroll
+    for (int l = 0; l < 5; ++l) R.Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
+    R.b0 = L[Y.oB + 10 * k + 2 * me];
+    R.b1 = L[Y.oB + 10 * k + 2 * me + 1];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) R.t[r] = L[odz + ZS * k + 5 + r];
+}
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
@@ -1014,55 +1046,56 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     if (REC_LANES(ln)) {
         const int me = (ln & 15) < 5 ? (ln & 15) : 4;
         double p = (ln & 15) < 5 ? L[ogl + ZS * N + me] : 0.0;
-        for (int k = N - 1; k >= 0; --k) {
-            double B0[5], B1[5], Lc[6], Ac[5], Kc[3];
-#pragma unroll
-            for (int l = 0; l < 5; ++l) {
-                B0[l] = L[Y.oB + 10 * k + 2 * l];
-                B1[l] = L[Y.oB + 10 * k + 2 * l + 1];
-                Ac[l] = L[Y.oA + 25 * k + 5 * l + me];
+        auto step = [&](const SolBk& c, int k) {
+            double h0 = c.h0, h1 = c.h1;
+            sol_h(h0, h1, p, c.B0, c.B1);
+            if (ln == 0) {
+                L[odz + ZS * k + 5] = h0;
+                L[odz + ZS * k + 6] = h1;
+                L[odz + ZS * k + 7] = c.h2;
             }
-#pragma unroll
-            for (int i = 0; i < 6; ++i) Lc[i] = L[Y.oL + 6 * k + i];
-#pragma unroll
-            for (int r = 0; r < 3; ++r) Kc[r] = L[Y.oK + 15 * k + 5 * r + me];
-            double h0 = L[ogl + ZS * k + 5], h1 = L[ogl + ZS * k + 6];
-            const double h2 = L[ogl + ZS * k + 7], gx = L[ogl + ZS * k + me];
-            sol_h(h0, h1, p, B0, B1);
-            double t[3] = {-h0, -h1, -h2};
-            chol3_solve(Lc, t);
-            if (ln == 0)
-#pragma unroll
-                for (int i = 0; i < 3; ++i) L[odz + ZS * k + 5 + i] = t[i];
-            if (k > 0) {
-                double v = gx;
-                dot5_lanes(v, p, Ac);
-                v = fma(Kc[0], h0, v);
-                v = fma(Kc[1], h1, v);
-                v = fma(Kc[2], h2, v);
-                p = v;
-            }
+            double v = c.gx;
+            dot5_lanes(v, p, c.Ac);
+            v = fma(c.Kc[0], h0, v);
+            v = fma(c.Kc[1], h1, v);
+            v = fma(c.Kc[2], c.h2, v);
+            p = v;
+        };
+        // two stages per trip, alternating buffers: each stage's loads are in flight during the other's work
+        SolBk ra, rb;
+        sol_load_bk(X, ogl, N - 1, me, ra);
+        int k = N - 1;
+        for (; k >= 1; k -= 2) {
+            sol_load_bk(X, ogl, k - 1, me, rb);
+            step(ra, k);
+            sol_load_bk(X, ogl, k >= 2 ? k - 2 : 0, me, ra);
+            step(rb, k - 1);
         }
+        if (k == 0) step(ra, 0);
     }
-    // the forward pass reads the feed-forward terms just stored
+    sync();
+    // feed-forward terms, stage-parallel: kk_k = -(L D L')^-1 h_k (oracle: the same chol3_solve per stage)
+    for (int k = ln; k < N; k += WAVE) {
+        double Lc[6], t[3];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Lc[i] = L[Y.oL + 6 * k + i];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) t[r] = -L[odz + ZS * k + 5 + r];
+        chol3_solve(Lc, t);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) L[odz + ZS * k + 5 + r] = t[r];
+    }
     sync();
     if (REC_LANES(ln)) {
         const int me = (ln & 15) < 5 ? (ln & 15) : 4;
         double x = 0.0;
-        for (int k = 0; k < N; ++k) {
-            double K[15], Ar[5], w[3];
-#pragma unroll
-            for (int i = 0; i < 15; ++i) K[i] = L[Y.oK + 15 * k + i];
-#pragma unroll
-            for (int l = 0; l < 5; ++l) Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
-            const double b0 = L[Y.oB + 10 * k + 2 * me], b1 = L[Y.oB + 10 * k + 2 * me + 1];
-#pragma unroll
-            for (int r = 0; r < 3; ++r) w[r] = L[odz + ZS * k + 5 + r];
-            sol_w(w, x, K);
+        auto step = [&](const SolFw& c, int k) {
+            double w[3] = {c.t[0], c.t[1], c.t[2]};
+            sol_w(w, x, c.K);
             double xn = 0.0;
-            dot5_lanes(xn, x, Ar);
-            xn = fma(b0, w[0], xn);
-            xn = fma(b1, w[1], xn);
+            dot5_lanes(xn, x, c.Ar);
+            xn = fma(c.b0, w[0], xn);
+            xn = fma(c.b1, w[1], xn);
             // stage k overwritten after every lane has read its feed-forward terms (program order within the
             // wave; the emulation's broadcasts above are barriers)
             if (ln < 5) L[odz + ZS * k + ln] = x;
@@ -1070,7 +1103,19 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
 #pragma unroll
                 for (int r = 0; r < 3; ++r) L[odz + ZS * k + 5 + r] = w[r];
             x = xn;
+        };
+        // two stages per trip, alternating buffers; a stage's feed-forward slots are read before the stage
+        // before it is overwritten (the loads are issued first)
+        SolFw fa, fb;
+        sol_load_fw(X, odz, 0, me, fa);
+        int k = 0;
+        for (; k + 1 < N; k += 2) {
+            sol_load_fw(X, odz, k + 1, me, fb);
+            step(fa, k);
+            sol_load_fw(X, odz, k + 2 < N ? k + 2 : k + 1, me, fa);
+            step(fb, k + 1);
         }
+        if (k < N) step(fa, k);
         if (ln < 5) L[odz + ZS * N + ln] = x;
         if (ln == 0)
 #pragma unroll
@@ -1116,31 +1161,37 @@ __device__ bool factor_par(const Ctx& X) {
             Pc[i] = ht(N, i);
             sel[i] = (j == i) ? 0.5 : 0.0;
         }
-        for (int k = N - 1; k >= 0; --k) {
-            double abc[5], m[8];
+        // one stage's inputs: column j of [A B], of HT (with delta) and HT(7, 7)
+        struct FacIn { double abc[5], m[8], h77; };
+        auto load = [&](int k, FacIn& R) {
 #pragma unroll
             for (int l = 0; l < 5; ++l)
-                abc[l] = j < 5 ? L[Y.oA + 25 * k + 5 * l + j] : (j < 7 ? L[Y.oB + 10 * k + 2 * l + (j - 5)] : 0.0);
+                R.abc[l] = j < 5 ? L[Y.oA + 25 * k + 5 * l + j] : (j < 7 ? L[Y.oB + 10 * k + 2 * l + (j - 5)] : 0.0);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) m[u] = ht(k, u);
-            const double h77 = L[Y.oHS + 8 * k + 7];
+            for (int u = 0; u < 8; ++u) R.m[u] = ht(k, u);
+            R.h77 = L[Y.oHS + 8 * k + 7];
+        };
+        auto step = [&](const FacIn& c, int k) -> bool {
+            double m[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) m[u] = c.m[u];
             double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-            fac_pab(q, Pc, abc);
-            fac_m(m, abc, q);
+            fac_pab(q, Pc, c.abc);
+            fac_m(m, c.abc, q);
             double t[3], Lc[6];
             fac_mww(t, m[5], m[6]);
             // chol3 of [[M55, ., .], [M65, M66, .], [0, 0, HT77]] (oracle chol3, same operations)
             const double d0 = t[0];
-            if (!(d0 > 0.0)) { okv = 0.0; break; }
+            if (!(d0 > 0.0)) return false;
             Lc[0] = 1.0 / d0;
             Lc[1] = t[1] * Lc[0];
             const double d1 = t[2] - Lc[1] * t[1];
-            if (!(d1 > 0.0)) { okv = 0.0; break; }
+            if (!(d1 > 0.0)) return false;
             Lc[2] = 1.0 / d1;
             Lc[3] = 0.0;
             Lc[4] = 0.0;
-            if (!(h77 > 0.0)) { okv = 0.0; break; }
-            Lc[5] = 1.0 / h77;
+            if (!(c.h77 > 0.0)) return false;
+            Lc[5] = 1.0 / c.h77;
             double kc[3] = {-m[5], -m[6], -m[7]};
             chol3_solve(Lc, kc);
             if (ln < 5)
@@ -1154,7 +1205,19 @@ __device__ bool factor_par(const Ctx& X) {
                 fac_pn(pn, m[5], m[6], m[7], kc);
                 fac_sym(Pc, pn, sel);
             }
+            return true;
+        };
+        // two stages per trip, alternating buffers: a stage's inputs are in flight during the other's work
+        FacIn fa, fb;
+        load(N - 1, fa);
+        int k = N - 1;
+        for (; k >= 1; k -= 2) {
+            load(k - 1, fb);
+            if (!step(fa, k)) { okv = 0.0; break; }
+            load(k >= 2 ? k - 2 : 0, fa);
+            if (!step(fb, k - 1)) { okv = 0.0; break; }
         }
+        if (okv != 0.0 && k == 0 && !step(fa, 0)) okv = 0.0;
         if (ln >= 8) okv = 1.0;          // the emulation's replicas of the recursion lanes
     }
     if (wmin(okv) == 0.0) return false;
