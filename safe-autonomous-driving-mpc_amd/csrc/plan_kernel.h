@@ -861,17 +861,28 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
 // term, so the two agree bit for bit.  The symmetrisation P <- (Pn + Pn') / 2 pairs lane j's column with the
 // row lane j needs from the other lanes by a per-lane selector (0.5 on the lane's own index, 0 elsewhere):
 // fma(0.5, Pn(j, i), 0.5 Pn(i, j)) = 0.5 (Pn(i, j) + Pn(j, i)) exactly (scaling by 2 commutes with rounding).
-// On the device the recursions run under an exec mask of lanes 0..7 (REC_LANES); the host emulation
-// (tools/plan_emu.cpp) runs them on every lane, since its broadcasts meet at a barrier of all 64 threads.
+// The recursions run on the whole wave (REC_LANES): the four 16-lane rows compute the same values (each
+// broadcast stays within its row; lanes 7..15 of a row carry a zero column) and only row 0 stores.  Narrowing
+// exec to lanes 0..7 made every FP64 instruction slower (tools/micro/dpp_lat.hip on the MI355X: v_fmac_f64
+// 5.4 -> 7.2 cycles, its DPP form 7.3 -> 9.5, a division 77 -> 100), so the replicas cost nothing and save
+// a quarter.  The host emulation (tools/plan_emu.cpp) runs every lane the same way.
 // ------------------------------------------------------------------------------------------------------
 
+// UNI(i): a wave-uniform int (an LDS offset of the context) in a scalar register.  The hot loops take their
+// offsets and scalars into locals first: the context lives in private memory and is reached through a
+// generic pointer in the non-inlined phases, which an LDS store may alias as far as the compiler knows, so
+// a field read inside a loop is a flat load (and a wait on it) per trip.
 #ifndef PLAN_HOST_EMU
-#define REC_LANES(ln) ((ln) < 8)
+#define UNI(i) __builtin_amdgcn_readfirstlane(i)
+#else
+#define UNI(i) (i)
+#endif
+
+#define REC_LANES(ln) true
+#ifndef PLAN_HOST_EMU
 // d += s@L * c: s broadcast from lane L of the 16-lane row (DPP row_newbcast), fused into the FMA.  Every asm
 // block starts with s_nop 1, the two wait states a DPP read needs after a VALU write of its source.
 #define PF(d, s, c, L) "v_fmac_f64_dpp " d ", " s ", " c " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"
-#else
-#define REC_LANES(ln) true
 #endif
 
 // acc += sum_l src@l * c[l] (l = 0..4, in that order): one lane's dot product with a vector held one
@@ -1137,23 +1148,18 @@ __device__ bool factor_par(const Ctx& X) {
     const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
+    const int oA = UNI(Y.oA), oB = UNI(Y.oB), oH = UNI(Y.oH), oHS = UNI(Y.oHS), oK = UNI(Y.oK), oL = UNI(Y.oL);
+    const double delta = X.delta;
     double okv = 1.0;
     if (REC_LANES(ln)) {
         const int j = (ln & 15) < 7 ? (ln & 15) : 7;
-        // per-lane address of HT(u, j): HS slot or packed H entry; dg: the diagonal entries H + delta I adds to
-        int hoff[8];
-        bool hsl[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int sl = hs_slot(u, j);
-            hsl[u] = sl >= 0;
-            hoff[u] = sl >= 0 ? sl : hidx(u, j);
-        }
-        const double dg1 = (j == 1) ? 1.0 : 0.0, dg2 = (j == 2) ? 1.0 : 0.0;
+        // HT(u, j) of stage k: the HS slot or the packed H entry (a per-lane base and stride, no branch); dg:
+        // the diagonal entries H + delta I adds to
         auto ht = [&](int k, int u) {
-            const double v = hsl[u] ? L[Y.oHS + 8 * k + hoff[u]] : L[Y.oH + HSTR * k + hoff[u]];
+            const int sl = hs_slot(u, j);
+            const double v = L[sl >= 0 ? oHS + sl + 8 * k : oH + hidx(u, j) + HSTR * k];
             // ht_at: (u == w && u < nv) ? h + delta : h for the non-slot diagonal entries (1, 1), (2, 2)
-            return u == 1 ? fma(dg1, X.delta, v) : (u == 2 ? fma(dg2, X.delta, v) : v);
+            return u == 1 ? fma(j == 1 ? 1.0 : 0.0, delta, v) : (u == 2 ? fma(j == 2 ? 1.0 : 0.0, delta, v) : v);
         };
         double Pc[5], sel[5];
 #pragma unroll
@@ -1161,15 +1167,20 @@ __device__ bool factor_par(const Ctx& X) {
             Pc[i] = ht(N, i);
             sel[i] = (j == i) ? 0.5 : 0.0;
         }
+        // column j of [A B] (lane 7: zeros), read at a per-lane base and strides
+        const int abase = j < 5 ? oA + j : (j < 7 ? oB + (j - 5) : oA), akst = j < 5 ? 25 : 10, alst = j < 5 ? 5 : 2;
+        const bool aon = j < 7;
         // one stage's inputs: column j of [A B], of HT (with delta) and HT(7, 7)
         struct FacIn { double abc[5], m[8], h77; };
         auto load = [&](int k, FacIn& R) {
 #pragma unroll
-            for (int l = 0; l < 5; ++l)
-                R.abc[l] = j < 5 ? L[Y.oA + 25 * k + 5 * l + j] : (j < 7 ? L[Y.oB + 10 * k + 2 * l + (j - 5)] : 0.0);
+            for (int l = 0; l < 5; ++l) {
+                const double v = L[abase + akst * k + alst * l];
+                R.abc[l] = aon ? v : 0.0;
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u) R.m[u] = ht(k, u);
-            R.h77 = L[Y.oHS + 8 * k + 7];
+            R.h77 = L[oHS + 8 * k + 7];
         };
         auto step = [&](const FacIn& c, int k) -> bool {
             double m[8];
@@ -1196,10 +1207,10 @@ __device__ bool factor_par(const Ctx& X) {
             chol3_solve(Lc, kc);
             if (ln < 5)
 #pragma unroll
-                for (int r = 0; r < 3; ++r) L[Y.oK + 15 * k + 5 * r + ln] = kc[r];
+                for (int r = 0; r < 3; ++r) L[oK + 15 * k + 5 * r + ln] = kc[r];
             if (ln == 0)
 #pragma unroll
-                for (int i = 0; i < 6; ++i) L[Y.oL + 6 * k + i] = Lc[i];
+                for (int i = 0; i < 6; ++i) L[oL + 6 * k + i] = Lc[i];
             if (k > 0) {
                 double pn[5] = {m[0], m[1], m[2], m[3], m[4]};
                 fac_pn(pn, m[5], m[6], m[7], kc);
@@ -1218,7 +1229,6 @@ __device__ bool factor_par(const Ctx& X) {
             if (!step(fb, k - 1)) { okv = 0.0; break; }
         }
         if (okv != 0.0 && k == 0 && !step(fa, 0)) okv = 0.0;
-        if (ln >= 8) okv = 1.0;          // the emulation's replicas of the recursion lanes
     }
     if (wmin(okv) == 0.0) return false;
     sync();
