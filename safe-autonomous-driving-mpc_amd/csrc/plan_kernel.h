@@ -132,10 +132,35 @@ __host__ __device__ Layout make_layout(int Nmax) {
     return y;
 }
 
+// UNI(i): a wave-uniform int (an LDS offset of the context) in a scalar register.  The hot loops take their
+// offsets and scalars into locals first: the context lives in private memory and is reached through a
+// generic pointer in the non-inlined phases, which an LDS store may alias as far as the compiler knows, so
+// a field read inside a loop is a flat load (and a wait on it) per trip.
+#ifndef PLAN_HOST_EMU
+#define UNI(i) __builtin_amdgcn_readfirstlane(i)
+#else
+#define UNI(i) (i)
+#endif
+// the layout's offsets, each in a scalar register (a hot function's copy of X.Y)
+__device__ inline Layout uni_layout(const Layout& y) {
+    Layout u;
+    u.NP = UNI(y.NP);
+    u.oA = UNI(y.oA); u.oB = UNI(y.oB); u.oC = UNI(y.oC); u.oH = UNI(y.oH); u.oHS = UNI(y.oHS);
+    u.oGQ = UNI(y.oGQ); u.oG = UNI(y.oG); u.oK = UNI(y.oK); u.oL = UNI(y.oL); u.oEZ = UNI(y.oEZ);
+    u.oZ = UNI(y.oZ); u.oS = UNI(y.oS); u.oLAM = UNI(y.oLAM); u.oGL = UNI(y.oGL); u.oDZ = UNI(y.oDZ);
+    u.oDSA = UNI(y.oDSA); u.oDLA = UNI(y.oDLA); u.oDS = UNI(y.oDS); u.oDL = UNI(y.oDL); u.oMY = UNI(y.oMY);
+    u.oMLAT = UNI(y.oMLAT); u.oZB = UNI(y.oZB); u.oZ2 = UNI(y.oZ2); u.oDZV = UNI(y.oDZV); u.oPI = UNI(y.oPI);
+    u.oVLIM = UNI(y.oVLIM); u.oVL = UNI(y.oVL); u.oACT = UNI(y.oACT); u.oTACT = UNI(y.oTACT); u.oSC = UNI(y.oSC);
+    u.oWK = UNI(y.oWK); u.oY = UNI(y.oY); u.oTLAM = UNI(y.oTLAM); u.oTZ = UNI(y.oTZ); u.total = UNI(y.total);
+    return u;
+}
+
 // phases of the diagnostic build
 enum { PH_OTHER, PH_BUILD, PH_HESS, PH_FACTOR, PH_SOLVE, PH_IPM, PH_EQP, PH_MULT, PH_LSEARCH, PH_ROLLOUT, PH_COUNT };
 // call counters of the diagnostic build (slots after the phases)
-enum { PH_NFACTOR = PH_COUNT, PH_NSOLVE, PH_NSLOTS };
+enum { PH_NFACTOR = PH_COUNT, PH_NSOLVE, PH_IGRAD, PH_IDIR, PH_IRED, PH_NSLOTS };   // slot 15: chunks
+// (PH_IGRAD / PH_IDIR / PH_IRED: the interior point's gradient rows, direction rows, and its reductions, ratio
+// tests and updates)
 
 // scalar slots (oSC + ...)
 enum { SC_DELTA, SC_NU0, SC_NU1, SC_EM0, SC_EM1, SC_EM2, SC_EM3, SC_FLAG };
@@ -518,6 +543,13 @@ struct PhScope {
     }
 };
 #define PHASE(p) PhScope ph_scope_(X, p)
+// an explicitly closed span (phases that are not a scope of their own)
+#define PhOpen(v, X, p) const unsigned long long v##_t0 = __builtin_amdgcn_s_memtime(); const int v##_p = (p)
+#define PhClose(v)                                                                                              \
+    do {                                                                                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                             \
+        if (X.ln == 0) *(PLAN_LDS_AS unsigned long long*)(X.L + X.Y.oSC + 16 + v##_p) += t_ - v##_t0;          \
+    } while (0)
 // calls of a phase (factorisations, solves), so that tools/plan_phase.py can report cycles per call and stage
 #define PROF_COUNT(p)                                                                        \
     do {                                                                                     \
@@ -526,6 +558,8 @@ struct PhScope {
 #else
 #define PHASE(p)
 #define PROF_COUNT(p)
+#define PhOpen(v, X, p)
+#define PhClose(v)
 #endif
 
 __device__ inline bool act_bit(const Ctx& X, int o, int k, int j) {
@@ -802,7 +836,7 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
     PHASE(PH_HESS);
     const int N = X.N;
     ldsd* L = X.L;
-    const Layout& Y = X.Y;
+    const Layout Y = uni_layout(X.Y);
     for (int k = X.ln; k <= N; k += WAVE) {
         // only the 8 entries rows touch are stored (hs_slot); the rest of the factorisation Hessian is
         // H + delta I, formed where it is read (ht_at)
@@ -867,16 +901,6 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
 // 5.4 -> 7.2 cycles, its DPP form 7.3 -> 9.5, a division 77 -> 100), so the replicas cost nothing and save
 // a quarter.  The host emulation (tools/plan_emu.cpp) runs every lane the same way.
 // ------------------------------------------------------------------------------------------------------
-
-// UNI(i): a wave-uniform int (an LDS offset of the context) in a scalar register.  The hot loops take their
-// offsets and scalars into locals first: the context lives in private memory and is reached through a
-// generic pointer in the non-inlined phases, which an LDS store may alias as far as the compiler knows, so
-// a field read inside a loop is a flat load (and a wait on it) per trip.
-#ifndef PLAN_HOST_EMU
-#define UNI(i) __builtin_amdgcn_readfirstlane(i)
-#else
-#define UNI(i) (i)
-#endif
 
 #define REC_LANES(ln) true
 #ifndef PLAN_HOST_EMU
@@ -1022,9 +1046,7 @@ __device__ inline void sol_w(double w[3], double x, const double K[15]) {
 // waits on no LDS read: what remains on its chain are the broadcast FMAs.  oracle solve_core().
 struct SolBk { double B0[5], B1[5], Ac[5], Kc[3], h0, h1, h2, gx; };
 struct SolFw { double K[15], Ar[5], b0, b1, t[3]; };
-__device__ inline void sol_load_bk(const Ctx& X, int ogl, int k, int me, SolBk& R) {
-    const ldsd* L = X.L;
-    const Layout& Y = X.Y;
+__device__ inline void sol_load_bk(const ldsd* L, const Layout& Y, int ogl, int k, int me, SolBk& R) {
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
         R.B0[l] = L[Y.oB + 10 * k + 2 * l];
@@ -1038,9 +1060,7 @@ __device__ inline void sol_load_bk(const Ctx& X, int ogl, int k, int me, SolBk& 
     R.h2 = L[ogl + ZS * k + 7];
     R.gx = L[ogl + ZS * k + me];
 }
-__device__ inline void sol_load_fw(const Ctx& X, int odz, int k, int me, SolFw& R) {
-    const ldsd* L = X.L;
-    const Layout& Y = X.Y;
+__device__ inline void sol_load_fw(const ldsd* L, const Layout& Y, int odz, int k, int me, SolFw& R) {
 #pragma unroll
     for (int i = 0; i < 15; ++i) R.K[i] = L[Y.oK + 15 * k + i];
 #pragma unroll
@@ -1053,7 +1073,7 @@ __device__ inline void sol_load_fw(const Ctx& X, int odz, int k, int me, SolFw& 
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
-    const Layout& Y = X.Y;
+    const Layout Y = uni_layout(X.Y);
     if (REC_LANES(ln)) {
         const int me = (ln & 15) < 5 ? (ln & 15) : 4;
         double p = (ln & 15) < 5 ? L[ogl + ZS * N + me] : 0.0;
@@ -1074,12 +1094,12 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         };
         // two stages per trip, alternating buffers: each stage's loads are in flight during the other's work
         SolBk ra, rb;
-        sol_load_bk(X, ogl, N - 1, me, ra);
+        sol_load_bk(L, Y, ogl, N - 1, me, ra);
         int k = N - 1;
         for (; k >= 1; k -= 2) {
-            sol_load_bk(X, ogl, k - 1, me, rb);
+            sol_load_bk(L, Y, ogl, k - 1, me, rb);
             step(ra, k);
-            sol_load_bk(X, ogl, k >= 2 ? k - 2 : 0, me, ra);
+            sol_load_bk(L, Y, ogl, k >= 2 ? k - 2 : 0, me, ra);
             step(rb, k - 1);
         }
         if (k == 0) step(ra, 0);
@@ -1118,12 +1138,12 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         // two stages per trip, alternating buffers; a stage's feed-forward slots are read before the stage
         // before it is overwritten (the loads are issued first)
         SolFw fa, fb;
-        sol_load_fw(X, odz, 0, me, fa);
+        sol_load_fw(L, Y, odz, 0, me, fa);
         int k = 0;
         for (; k + 1 < N; k += 2) {
-            sol_load_fw(X, odz, k + 1, me, fb);
+            sol_load_fw(L, Y, odz, k + 1, me, fb);
             step(fa, k);
-            sol_load_fw(X, odz, k + 2 < N ? k + 2 : k + 1, me, fa);
+            sol_load_fw(L, Y, odz, k + 2 < N ? k + 2 : k + 1, me, fa);
             step(fb, k + 1);
         }
         if (k < N) step(fa, k);
@@ -1282,7 +1302,7 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     PHASE(PH_SOLVE);
     PROF_COUNT(PH_NSOLVE);
     ldsd* L = X.L;
-    const Layout& Y = X.Y;
+    const Layout Y = uni_layout(X.Y);
     const int N = X.N;
     solve_core(X, Y.oGL, Y.oDZ);
     sync();
@@ -1311,7 +1331,7 @@ __device__ void rollout(const Ctx& X, int oz) {
     PHASE(PH_ROLLOUT);
     const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
-    const Layout& Y = X.Y;
+    const Layout Y = uni_layout(X.Y);
     if (REC_LANES(ln)) {
         const int me = (ln & 15) < 5 ? (ln & 15) : 4;
         double x = X.xi0[me];
@@ -1355,7 +1375,7 @@ __device__ int eqp(Ctx& X, double scale) {
     PHASE(PH_EQP);
     const int N = X.N;
     ldsd* L = X.L;
-    const Layout& Y = X.Y;
+    const Layout Y = uni_layout(X.Y);
     for (int k = X.ln; k <= N; k += WAVE)
 #pragma unroll
         for (int j = 0; j < NR; ++j) L[Y.oY + NR * k + j] = act_bit(X, Y.oTACT, k, j) ? L[Y.oTLAM + NR * k + j] : 0.0;
@@ -1447,7 +1467,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     PHASE(PH_IPM);
     const int N = X.N;
     ldsd* L = X.L;
-    const Layout& Y = X.Y;
+    const Layout Y = uni_layout(X.Y);
     if (!resume) rollout(X, Y.oZ);
     int m = 0;
     for (int k = X.ln; k <= N; k += WAVE) {
@@ -1472,6 +1492,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     int it = resume ? *iters : 0, rc = 1;
     for (; it < X.P.max_iter; ++it) {
         double mu = 0.0;
+        PhOpen(ph_red, X, PH_IRED);
         for (int k = X.ln; k <= N; k += WAVE) {
             const int nr = stage_nrows(k, N, X.fin);
 #pragma unroll
@@ -1481,6 +1502,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             }
         }
         mu = wsum(mu) / m;
+        PhClose(ph_red);
         if (!isfinite(mu)) { rc = -1; break; }
         if (mu <= X.P.tol && phi <= 1e-12) { rc = 0; break; }
         if (!resume && mu <= MU_CHECK && phi <= MU_CHECK) {
@@ -1501,6 +1523,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
             if (pass == 1) {
+                PhOpen(ph_r1, X, PH_IRED);
                 double am = 1.0;
                 for (int k = X.ln; k <= N; k += WAVE) {
                     const int nr = stage_nrows(k, N, X.fin);
@@ -1526,7 +1549,9 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 mua = wsum(mua) / m;
                 const double ratio = mua / mu;
                 sigma_mu = ratio * ratio * ratio * mu;
+                PhClose(ph_r1);
             }
+            PhOpen(ph_g, X, PH_IGRAD);
             for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 2) & 1); ++rp_)
             for (int k = X.ln; k <= N; k += WAVE) {
                 double g[NZ], z[NZ];
@@ -1552,9 +1577,11 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
             }
             sync();
+            PhClose(ph_g);
             if (X.dbg & 2) solve(X, rE);
             solve(X, rE);
             const int ods = pass == 0 ? Y.oDSA : Y.oDS, odl = pass == 0 ? Y.oDLA : Y.oDL;
+            PhOpen(ph_d, X, PH_IDIR);
             for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 3) & 1); ++rp_)
             for (int k = X.ln; k <= N; k += WAVE) {
                 double z[NZ], dz[NZ];
@@ -1580,7 +1607,9 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 });
             }
             sync();
+            PhClose(ph_d);
         }
+        PhOpen(ph_r2, X, PH_IRED);
         double amax = 1.0 / TAU, fin = 1.0;
         for (int k = X.ln; k <= N; k += WAVE) {
             const int nr = stage_nrows(k, N, X.fin);
@@ -1613,6 +1642,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             }
         }
         sync();
+        PhClose(ph_r2);
         phi *= 1.0 - alpha;
     }
     sync();

@@ -49,6 +49,9 @@ def profile(pl, label, N, x0, st, fin):
         it = float(g["iters"].sum())
         if it:
             print(f"  per interior-point iteration (all phases): {tot / it:.0f} cycles", flush=True)
+            sub = np.array(buf[len(PHASES) + 2:len(PHASES) + 5], dtype=np.float64)
+            print(f"  interior point per iteration: gradient rows {sub[0] / it:.0f}, direction rows {sub[1] / it:.0f}, "
+                  f"reductions/ratio tests/update {sub[2] / it:.0f} cycles", flush=True)
 
 
 if sys.argv[1] == "bench":
