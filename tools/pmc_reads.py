@@ -1,10 +1,15 @@
 """Summary of tools/gpu_r05_pmc_reads.sh: per-dispatch counter means of the C2 solver kernels (crossover
 MODE_XO, interior point MODE_IPM) for each pass, and a linear fit over B of FETCH_SIZE per kernel (per-launch
-intercept vs per-instance slope).  Writes profiles/r05_pmc_reads.csv and prints a table."""
+intercept vs per-instance slope).  Writes profiles/r05_pmc_reads.csv and prints a table, then the attribution: each kernel's code-object
+size (C2: MODE_IPM / MODE_XO instantiation at N = 20 without obstacles) times the 8 XCDs, whose L2s each
+fetch the code once per launch, against the per-launch intercept."""
 import csv
 import glob
 import os
 import re
+
+import subprocess
+import tempfile
 
 import numpy as np
 
@@ -36,6 +41,27 @@ def pass_means(tag):
     return {k: (float(np.mean(v)), len(v)) for k, v in res.items()}
 
 
+def code_sizes(so_path):
+    """{mode: bytes} of the C2 kernels (mpc_solve_kernel<32, false, mode, 20>) in the library's gfx950 code object"""
+    llvm = "/opt/rocm/lib/llvm/bin"
+    with tempfile.TemporaryDirectory() as d:
+        fat, co = os.path.join(d, "fatbin"), os.path.join(d, "dev.co")
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", so_path, os.path.join(d, "x")],
+                       check=True, capture_output=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+        syms = subprocess.run([f"{llvm}/llvm-readelf", "-s", "--wide", co], check=True, capture_output=True,
+                              text=True).stdout
+    out = {}
+    for line in syms.splitlines():
+        f = line.split()
+        if len(f) >= 8 and f[3] == "FUNC":
+            m = re.search(r"mpc_solve_kernelILi32ELb0ELi(\d)ELi20E", f[7])
+            if m:
+                out[{"1": "XO", "2": "IPM"}.get(m.group(1), m.group(1))] = int(f[2])
+    return out
+
+
 def main():
     rows = []
     fits = {}
@@ -62,6 +88,16 @@ def main():
             slope, icpt = np.polyfit(b, v, 1)
             print(f"FETCH_SIZE fit {md}: {icpt:.1f} KiB per launch + {slope * 1024:.1f} B per instance "
                   f"(KiB as counted; x2 for 128-B requests tallied at 64 B)")
+    so = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcqp.so")
+    if os.path.exists(so):
+        cs = code_sizes(so)
+        tot = {md: dict(pts)[4096] for md, pts in fits.items() if 4096 in dict(pts)}
+        code = {md: 8 * cs.get(md, 0) / 1024 for md in tot}
+        for md in tot:
+            print(f"{md}: code object {cs.get(md, 0)} B x 8 XCDs = {code[md]:.0f} KiB of {tot[md]:.0f} KiB counted at "
+                  f"B = 4096 ({code[md] / tot[md] * 100:.0f}%)")
+        print(f"both kernels: code {sum(code.values()):.0f} KiB of {sum(tot.values()):.0f} KiB counted "
+              f"({sum(code.values()) / sum(tot.values()) * 100:.0f}%)")
 
 
 if __name__ == "__main__":
