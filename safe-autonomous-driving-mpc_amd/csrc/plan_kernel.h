@@ -433,6 +433,42 @@ __device__ inline double sp_dot(const RowSp& r, double g, const double z[NZ]) {
     return v;
 }
 
+// Row-parallel visits: slot q = NR k + j of the row arrays (S, LAM, G, DS, ...), lane q, q + 64, ...: the
+// interior point's per-row divisions and ratio tests run on (N + 1) NR / 64 slots per lane instead of a
+// stage's NR rows on each of N + 1 lanes.  The row's stage, kind and coefficients come arithmetically from
+// q (no branch per kind): the same values row_sp gives (c0 = -vb vb for ROW_LATP is (-vb) vb exactly,
+// c1 = (-2 kb) vb likewise), so every row value is formed by the same operations as in for_rows.
+struct RowAt {
+    int k, i0, i1;
+    bool on, two;
+    double c0, c1;
+};
+__device__ inline RowAt row_at(const ldsd* L, int oZB, int q, int N, int fin) {
+    RowAt r;
+    const int k = q / NR, j = q - NR * k;
+    r.k = k;
+    const int n0 = (fin && k == N) ? 0 : (k > 0 ? 4 : 2);
+    const int n1 = k > 0 ? 2 : 0;
+    const int n2 = k < N ? 5 : 0;
+    const int n3 = (k == N && !fin) ? 1 : 0;
+    r.on = j < n0 + n1 + n2 + n3;
+    const int kind = j < n0 ? j : (j < n0 + n1 ? ROW_KMIN + (j - n0) : (j < n0 + n1 + n2 ? ROW_U1MIN + (j - n0 - n1) : ROW_STERM));
+    // nibble tables over the kinds (ROW_VMIN .. ROW_STERM): first and second coefficient's variable
+    constexpr unsigned long long I0TAB = 0x076655333344ull;   // kind 0..11: 4 4 3 3 3 3 5 5 6 6 7 0
+    constexpr unsigned long long I1TAB = 0x076655334477ull;   // kind 0..11: 7 7 4 4 3 3 5 5 6 6 7 0
+    r.i0 = (int)((I0TAB >> (4 * kind)) & 15ull);
+    r.i1 = (int)((I1TAB >> (4 * kind)) & 15ull);
+    const bool neg = (0x2A6u >> kind) & 1u;                            // VMAX, LATP, KMAX, U1MAX, U2MAX
+    const bool lat = kind == ROW_LATP || kind == ROW_LATM;
+    r.two = lat || (kind <= ROW_VMAX && k < N);
+    const double kb = L[oZB + ZS * k + 3], vb = L[oZB + ZS * k + 4];
+    const double vv = neg ? -vb * vb : vb * vb;
+    r.c0 = lat ? vv : (neg ? -1.0 : 1.0);
+    const double kk2 = neg ? -2.0 * kb : 2.0 * kb;
+    r.c1 = lat ? kk2 * vb : (neg ? -1.0 : 1.0);
+    return r;
+}
+
 // Gaussian elimination with partial pivoting on a 5x5 system with NC right-hand sides (registers)
 template <int NC>
 __device__ bool solve5(double M[25], double R[5 * NC]) {
@@ -837,6 +873,16 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
     const int N = X.N;
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
+    if (mode == 0) {
+        // the barrier weights w = lam / s, row-parallel, into DS (free at the top of an interior-point
+        // iteration: the previous step has been taken)
+        for (int q = X.ln; q < (N + 1) * NR; q += WAVE) {
+            const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+            const double w = L[Y.oLAM + q] / L[Y.oS + q];
+            if (r.on) L[Y.oDS + q] = w;
+        }
+        sync();
+    }
     for (int k = X.ln; k <= N; k += WAVE) {
         // only the 8 entries rows touch are stored (hs_slot); the rest of the factorisation Hessian is
         // H + delta I, formed where it is read (ht_at)
@@ -858,7 +904,7 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         const unsigned act = mode == 0 ? 0u : (unsigned)L[Y.oTACT + k];
         for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
-            const double w = mode == 0 ? L[Y.oLAM + NR * k + j] / L[Y.oS + NR * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
+            const double w = mode == 0 ? L[Y.oDS + NR * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
             const bool use = on && w != 0.0;
             const RowSp r = row_sp(kind, k < N, kb, vb);
             const int a = hx(r.i0, r.i0), b = hx(r.i0, r.i1), c = hx(r.i1, r.i1);
@@ -1468,6 +1514,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     const int N = X.N;
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
+    const int nq = (N + 1) * NR, nzq = (N + 1) * ZS;      // row slots, stage-variable slots
     if (!resume) rollout(X, Y.oZ);
     int m = 0;
     for (int k = X.ln; k <= N; k += WAVE) {
@@ -1507,13 +1554,10 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         if (mu <= X.P.tol && phi <= 1e-12) { rc = 0; break; }
         if (!resume && mu <= MU_CHECK && phi <= MU_CHECK) {
             double tie = 0.0;
-            for (int k = X.ln; k <= N; k += WAVE) {
-                const int nr = stage_nrows(k, N, X.fin);
-#pragma unroll
-                for (int j = 0; j < NR; ++j) {
-                    const double sv = L[Y.oS + NR * k + j], lv = L[Y.oLAM + NR * k + j];
-                    if (j < nr && !(sv > CHECK_SEP * lv || lv > CHECK_SEP * sv)) tie = 1.0;
-                }
+            for (int q = X.ln; q < nq; q += WAVE) {
+                const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                const double sv = L[Y.oS + q], lv = L[Y.oLAM + q];
+                if (r.on && !(sv > CHECK_SEP * lv || lv > CHECK_SEP * sv)) tie = 1.0;
             }
             if (wmax(tie) == 0.0) { rc = 2; break; }
         }
@@ -1525,15 +1569,12 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             if (pass == 1) {
                 PhOpen(ph_r1, X, PH_IRED);
                 double am = 1.0;
-                for (int k = X.ln; k <= N; k += WAVE) {
-                    const int nr = stage_nrows(k, N, X.fin);
-#pragma unroll
-                    for (int j = 0; j < NR; ++j) {
-                        const double dsa = L[Y.oDSA + NR * k + j], dla = L[Y.oDLA + NR * k + j];
-                        const double rs = -L[Y.oS + NR * k + j] / dsa, rl = -L[Y.oLAM + NR * k + j] / dla;
-                        am = (j < nr && dsa < 0.0) ? fmin(am, rs) : am;
-                        am = (j < nr && dla < 0.0) ? fmin(am, rl) : am;
-                    }
+                for (int q = X.ln; q < nq; q += WAVE) {
+                    const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                    const double dsa = L[Y.oDSA + q], dla = L[Y.oDLA + q];
+                    const double rs = -L[Y.oS + q] / dsa, rl = -L[Y.oLAM + q] / dla;
+                    am = (r.on && dsa < 0.0) ? fmin(am, rs) : am;
+                    am = (r.on && dla < 0.0) ? fmin(am, rl) : am;
                 }
                 am = wmin(am);
                 double mua = 0.0;
@@ -1552,29 +1593,40 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 PhClose(ph_r1);
             }
             PhOpen(ph_g, X, PH_IGRAD);
-            for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 2) & 1); ++rp_)
-            for (int k = X.ln; k <= N; k += WAVE) {
-                double g[NZ], z[NZ];
-                grad_f(X, k, Y.oZ, g);
-#pragma unroll
-                for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
-                const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-                for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
-                    const RowSp r = row_sp(kind, k < N, kb, vb);
-                    const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
+            for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 2) & 1); ++rp_) {
+                // each row's f = l + (rs - l rp) / s, row-parallel, into DS (free until this pass's
+                // direction rows write it); then each stage folds its rows into the gradient in row order
+                for (int q = X.ln; q < nq; q += WAVE) {
+                    const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                    const double s = L[Y.oS + q], l = L[Y.oLAM + q];
                     double rs = -s * l;
-                    if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
-                    const double rp = sp_dot(r, L[Y.oG + NR * k + j], z) - s;
+                    if (pass == 1) rs += sigma_mu - L[Y.oDSA + q] * L[Y.oDLA + q];
+                    double sp = L[Y.oG + q] + r.c0 * L[Y.oZ + ZS * r.k + r.i0];
+                    const double sp2 = sp + r.c1 * L[Y.oZ + ZS * r.k + r.i1];
+                    sp = r.two ? sp2 : sp;
+                    const double rp = sp - s;
                     const double f = l + (rs - l * rp) / s;
-                    const double g0 = g[r.i0] - f * r.c0;
-                    g[r.i0] = on ? g0 : g[r.i0];
-                    if (r.two) {
-                        const double g1 = g[r.i1] - f * r.c1;
-                        g[r.i1] = on ? g1 : g[r.i1];
-                    }
-                });
+                    if (r.on) L[Y.oDS + q] = f;
+                }
+                sync();
+                for (int k = X.ln; k <= N; k += WAVE) {
+                    double g[NZ];
+                    grad_f(X, k, Y.oZ, g);
+                    const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
+                    for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+                        const RowSp r = row_sp(kind, k < N, kb, vb);
+                        const double f = L[Y.oDS + NR * k + j];
+                        const double g0 = g[r.i0] - f * r.c0;
+                        g[r.i0] = on ? g0 : g[r.i0];
+                        if (r.two) {
+                            const double g1 = g[r.i1] - f * r.c1;
+                            g[r.i1] = on ? g1 : g[r.i1];
+                        }
+                    });
 #pragma unroll
-                for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
+                    for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
+                }
+                sync();
             }
             sync();
             PhClose(ph_g);
@@ -1583,62 +1635,52 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             const int ods = pass == 0 ? Y.oDSA : Y.oDS, odl = pass == 0 ? Y.oDLA : Y.oDL;
             PhOpen(ph_d, X, PH_IDIR);
             for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 3) & 1); ++rp_)
-            for (int k = X.ln; k <= N; k += WAVE) {
-                double z[NZ], dz[NZ];
-#pragma unroll
-                for (int u = 0; u < NZ; ++u) {
-                    z[u] = L[Y.oZ + ZS * k + u];
-                    dz[u] = L[Y.oDZ + ZS * k + u];
+            for (int q = X.ln; q < nq; q += WAVE) {
+                const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                const double s = L[Y.oS + q], l = L[Y.oLAM + q];
+                double rs = -s * l;
+                if (pass == 1) rs += sigma_mu - L[Y.oDSA + q] * L[Y.oDLA + q];
+                const int zk = ZS * r.k;
+                double v = L[Y.oG + q] + r.c0 * L[Y.oZ + zk + r.i0];
+                const double v2 = v + r.c1 * L[Y.oZ + zk + r.i1];
+                v = r.two ? v2 : v;
+                v -= s;
+                v += r.c0 * L[Y.oDZ + zk + r.i0];
+                const double v3 = v + r.c1 * L[Y.oDZ + zk + r.i1];
+                v = r.two ? v3 : v;
+                const double dl = (rs - l * v) / s;
+                if (r.on) {
+                    L[ods + q] = v;
+                    L[odl + q] = dl;
                 }
-                const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-                for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
-                    const RowSp r = row_sp(kind, k < N, kb, vb);
-                    const double s = L[Y.oS + NR * k + j], l = L[Y.oLAM + NR * k + j];
-                    double rs = -s * l;
-                    if (pass == 1) rs += sigma_mu - L[Y.oDSA + NR * k + j] * L[Y.oDLA + NR * k + j];
-                    double v = sp_dot(r, L[Y.oG + NR * k + j], z) - s;
-                    v += r.c0 * dz[r.i0];
-                    if (r.two) v += r.c1 * dz[r.i1];
-                    const double dl = (rs - l * v) / s;
-                    if (on) {
-                        L[ods + NR * k + j] = v;
-                        L[odl + NR * k + j] = dl;
-                    }
-                });
             }
             sync();
             PhClose(ph_d);
         }
         PhOpen(ph_r2, X, PH_IRED);
         double amax = 1.0 / TAU, fin = 1.0;
-        for (int k = X.ln; k <= N; k += WAVE) {
-            const int nr = stage_nrows(k, N, X.fin);
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {
-                const double ds = L[Y.oDS + NR * k + j], dl = L[Y.oDL + NR * k + j];
-                const double rs = -L[Y.oS + NR * k + j] / ds, rl = -L[Y.oLAM + NR * k + j] / dl;
-                amax = (j < nr && ds < 0.0) ? fmin(amax, rs) : amax;
-                amax = (j < nr && dl < 0.0) ? fmin(amax, rl) : amax;
-            }
-#pragma unroll
-            for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oDZ + ZS * k + u]) ? fin : 0.0;
+        for (int q = X.ln; q < nq; q += WAVE) {
+            const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+            const double ds = L[Y.oDS + q], dl = L[Y.oDL + q];
+            const double rs = -L[Y.oS + q] / ds, rl = -L[Y.oLAM + q] / dl;
+            amax = (r.on && ds < 0.0) ? fmin(amax, rs) : amax;
+            amax = (r.on && dl < 0.0) ? fmin(amax, rl) : amax;
         }
+        for (int q = X.ln; q < nzq; q += WAVE)
+            if (q % ZS < NZ) fin = isfinite(L[Y.oDZ + q]) ? fin : 0.0;
         amax = wmin(amax);
         fin = wmin(fin);
         const double alpha = fmin(1.0, TAU * amax);
         if (!isfinite(alpha) || fin == 0.0) { rc = -1; break; }
-        for (int k = X.ln; k <= N; k += WAVE) {
-#pragma unroll
-            for (int u = 0; u < NZ; ++u) L[Y.oZ + ZS * k + u] += alpha * L[Y.oDZ + ZS * k + u];
-            const int nr = stage_nrows(k, N, X.fin);
-#pragma unroll
-            for (int j = 0; j < NR; ++j) {
-                const double sn = L[Y.oS + NR * k + j] + alpha * L[Y.oDS + NR * k + j];
-                const double ln_ = L[Y.oLAM + NR * k + j] + alpha * L[Y.oDL + NR * k + j];
-                if (j < nr) {
-                    L[Y.oS + NR * k + j] = sn;
-                    L[Y.oLAM + NR * k + j] = ln_;
-                }
+        for (int q = X.ln; q < nzq; q += WAVE)
+            if (q % ZS < NZ) L[Y.oZ + q] += alpha * L[Y.oDZ + q];
+        for (int q = X.ln; q < nq; q += WAVE) {
+            const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+            const double sn = L[Y.oS + q] + alpha * L[Y.oDS + q];
+            const double ln_ = L[Y.oLAM + q] + alpha * L[Y.oDL + q];
+            if (r.on) {
+                L[Y.oS + q] = sn;
+                L[Y.oLAM + q] = ln_;
             }
         }
         sync();

@@ -97,7 +97,43 @@ static std::vector<T> rd(FILE* f, size_t n) {
     return v;
 }
 
+// --rows: the row-parallel slot decoding (row_at) against the per-stage visit (for_rows / row_sp) for every
+// horizon, both chunk kinds and every slot: stage, presence, variables and coefficients bit for bit
+static int rows_selftest() {
+    std::vector<double> L(8 * 80 * ZS, 0.0);
+    int bad = 0, checked = 0;
+    for (int N = 1; N <= 64; ++N)
+        for (int fin = 0; fin < 2; ++fin) {
+            for (int k = 0; k <= N; ++k) {
+                L[ZS * k + 3] = 0.37 * (k + 1) - 2.1;           // kb
+                L[ZS * k + 4] = 1.3 + 0.71 * k;                  // vb
+            }
+            for (int k = 0; k <= N; ++k) {
+                bool seen[NR] = {false};
+                const double kb = L[ZS * k + 3], vb = L[ZS * k + 4];
+                for_rows(k, N, fin, [&](int kind, int j, bool on) {
+                    if (!on) return;
+                    seen[j] = true;
+                    const RowSp r = row_sp(kind, k < N, kb, vb);
+                    const RowAt a = row_at(L.data(), 0, NR * k + j, N, fin);
+                    ++checked;
+                    const bool ok = a.k == k && a.on && a.i0 == r.i0 && a.two == r.two &&
+                                    std::memcmp(&a.c0, &r.c0, 8) == 0 && (!r.two || (a.i1 == r.i1 && std::memcmp(&a.c1, &r.c1, 8) == 0));
+                    if (!ok && bad++ < 10)
+                        fprintf(stderr, "N=%d fin=%d k=%d j=%d kind=%d: row_at k %d i0 %d i1 %d two %d c0 %g c1 %g vs i0 %d i1 %d two %d c0 %g c1 %g\n",
+                                N, fin, k, j, kind, a.k, a.i0, a.i1, a.two, a.c0, a.c1, r.i0, r.i1, r.two, r.c0, r.c1);
+                });
+                for (int j = 0; j < NR; ++j)
+                    if (!seen[j] && row_at(L.data(), 0, NR * k + j, N, fin).on && bad++ < 10)
+                        fprintf(stderr, "N=%d fin=%d k=%d j=%d: row_at says on, for_rows has no row there\n", N, fin, k, j);
+            }
+        }
+    printf("rows selftest: %d rows checked, %d mismatches\n", checked, bad);
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 2 && std::strcmp(argv[1], "--rows") == 0) return rows_selftest();
     if (argc < 3) {
         fprintf(stderr, "usage: %s in.bin out.bin [first count]\n", argv[0]);
         return 2;
