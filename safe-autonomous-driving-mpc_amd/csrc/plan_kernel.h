@@ -141,19 +141,9 @@ __host__ __device__ Layout make_layout(int Nmax) {
 #else
 #define UNI(i) (i)
 #endif
-// the layout's offsets, each in a scalar register (a hot function's copy of X.Y)
-__device__ inline Layout uni_layout(const Layout& y) {
-    Layout u;
-    u.NP = UNI(y.NP);
-    u.oA = UNI(y.oA); u.oB = UNI(y.oB); u.oC = UNI(y.oC); u.oH = UNI(y.oH); u.oHS = UNI(y.oHS);
-    u.oGQ = UNI(y.oGQ); u.oG = UNI(y.oG); u.oK = UNI(y.oK); u.oL = UNI(y.oL); u.oEZ = UNI(y.oEZ);
-    u.oZ = UNI(y.oZ); u.oS = UNI(y.oS); u.oLAM = UNI(y.oLAM); u.oGL = UNI(y.oGL); u.oDZ = UNI(y.oDZ);
-    u.oDSA = UNI(y.oDSA); u.oDLA = UNI(y.oDLA); u.oDS = UNI(y.oDS); u.oDL = UNI(y.oDL); u.oMY = UNI(y.oMY);
-    u.oMLAT = UNI(y.oMLAT); u.oZB = UNI(y.oZB); u.oZ2 = UNI(y.oZ2); u.oDZV = UNI(y.oDZV); u.oPI = UNI(y.oPI);
-    u.oVLIM = UNI(y.oVLIM); u.oVL = UNI(y.oVL); u.oACT = UNI(y.oACT); u.oTACT = UNI(y.oTACT); u.oSC = UNI(y.oSC);
-    u.oWK = UNI(y.oWK); u.oY = UNI(y.oY); u.oTLAM = UNI(y.oTLAM); u.oTZ = UNI(y.oTZ); u.total = UNI(y.total);
-    return u;
-}
+// the layout's offsets in scalar registers (a hot function's copy of X.Y): recomputed from the uniform Nmax
+// (make_layout is integer arithmetic), one private-memory read instead of one per field
+__device__ inline Layout uni_layout(const Layout& y) { return make_layout(UNI(y.NP) - 1); }
 
 // phases of the diagnostic build
 enum { PH_OTHER, PH_BUILD, PH_HESS, PH_FACTOR, PH_SOLVE, PH_IPM, PH_EQP, PH_MULT, PH_LSEARCH, PH_ROLLOUT, PH_COUNT };
@@ -381,7 +371,7 @@ __device__ inline int row_kind(int k, int N, int fin, int j) {
 // (for_rows), where each kind, and with it the indices of its nonzero coefficients, is a compile-time
 // constant.  Adding only the nonzero terms, in the same order, gives the dense loops' values (a skipped
 // term is an exact zero).
-__device__ inline bool row_on(int kind, int k, int N, int fin) {
+__device__ __forceinline__ bool row_on(int kind, int k, int N, int fin) {
     switch (kind) {
         case ROW_VMIN: case ROW_VMAX: return !(fin && k == N);
         case ROW_LATP: case ROW_LATM: return !(fin && k == N) && k > 0;
@@ -395,7 +385,7 @@ struct RowSp {
     double c0, c1;
     bool two;            // c1 present
 };
-__device__ inline RowSp row_sp(int kind, bool has_w, double kb, double vb) {
+__device__ __forceinline__ RowSp row_sp(int kind, bool has_w, double kb, double vb) {
     switch (kind) {
         case ROW_VMIN: return {4, 7, 1.0, 1.0, has_w};
         case ROW_VMAX: return {4, 7, -1.0, -1.0, has_w};
@@ -416,18 +406,22 @@ __device__ inline RowSp row_sp(int kind, bool has_w, double kb, double vb) {
 // unconditionally -- loads, divisions and all -- and applies its results under `on` (selects, masked stores):
 // no branch per kind, so the scheduler overlaps the rows' independent chains (one lane serves a stage, so
 // the rows are its serial work); every on-row value is computed by the same operations as before.
-template <class F>
-__device__ inline void for_rows(int k, int N, int fin, F&& f) {
-    int j = 0;
-#pragma unroll
-    for (int kind = 0; kind <= ROW_STERM; ++kind) {
-        const bool on = row_on(kind, k, N, fin);
-        f(kind, j < NR ? j : NR - 1, on);
-        j += on ? 1 : 0;
+// (a compile-time recursion over the kinds: a loop the unroller gives up on in a large function would index
+// the callers' per-lane arrays at run time, which puts them in scratch memory)
+template <int KIND, class F>
+__device__ __forceinline__ void for_rows_from(int k, int N, int fin, int j, F& f) {
+    if constexpr (KIND <= ROW_STERM) {
+        const bool on = row_on(KIND, k, N, fin);
+        f(KIND, j < NR ? j : NR - 1, on);
+        for_rows_from<KIND + 1>(k, N, fin, j + (on ? 1 : 0), f);
     }
 }
+template <class F>
+__device__ __forceinline__ void for_rows(int k, int N, int fin, F&& f) {
+    for_rows_from<0>(k, N, fin, 0, f);
+}
 // g + a . z
-__device__ inline double sp_dot(const RowSp& r, double g, const double z[NZ]) {
+__device__ __forceinline__ double sp_dot(const RowSp& r, double g, const double z[NZ]) {
     double v = g + r.c0 * z[r.i0];
     if (r.two) v += r.c1 * z[r.i1];
     return v;
@@ -1048,104 +1042,74 @@ __device__ inline void fac_sym(double s[5], const double pn[5], const double sel
 #endif
 }
 
-// two components of the co-state's control rhs in every lane: h[r] += sum_l B(l, r) p_l (B uniform, p_l of lane l)
-__device__ inline void sol_h(double& h0, double& h1, double p, const double B0[5], const double B1[5]) {
+// acc += src@0 * c0 + src@1 * c1 (in that order): the lanes 0 and 1 components of a vector held one component
+// per lane, into every lane's sum (the solves' B w and K' h terms)
+__device__ inline void dot2_lanes(double& acc, double src, double c0, double c1) {
 #ifndef PLAN_HOST_EMU
-    asm("s_nop 1\n\t" PF("%0", "%2", "%3", 0) PF("%1", "%2", "%8", 0) PF("%0", "%2", "%4", 1) PF("%1", "%2", "%9", 1)
-        PF("%0", "%2", "%5", 2) PF("%1", "%2", "%10", 2) PF("%0", "%2", "%6", 3) PF("%1", "%2", "%11", 3)
-        PF("%0", "%2", "%7", 4) PF("%1", "%2", "%12", 4)
-        : "+&v"(h0), "+&v"(h1)
-        : "v"(p), "v"(B0[0]), "v"(B0[1]), "v"(B0[2]), "v"(B0[3]), "v"(B0[4]), "v"(B1[0]), "v"(B1[1]), "v"(B1[2]),
-          "v"(B1[3]), "v"(B1[4]));
+    asm("s_nop 1\n\t" PF("%0", "%1", "%2", 0) PF("%0", "%1", "%3", 1) : "+&v"(acc) : "v"(src), "v"(c0), "v"(c1));
 #else
-    for (int l = 0; l < 5; ++l) {
-        const double pl = dpp_row_bcast(p, l);
-        h0 = fma(pl, B0[l], h0);
-        h1 = fma(pl, B1[l], h1);
-    }
-#endif
-}
-
-// the feedback controls in every lane: w[r] += sum_l K(r, l) x_l (K uniform, x_l of lane l)
-__device__ inline void sol_w(double w[3], double x, const double K[15]) {
-#ifndef PLAN_HOST_EMU
-#define W_L(L, A, B, C) PF("%0", "%3", A, L) PF("%1", "%3", B, L) PF("%2", "%3", C, L)
-    asm("s_nop 1\n\t" W_L(0, "%4", "%9", "%14") W_L(1, "%5", "%10", "%15") W_L(2, "%6", "%11", "%16")
-        W_L(3, "%7", "%12", "%17") W_L(4, "%8", "%13", "%18")
-        : "+&v"(w[0]), "+&v"(w[1]), "+&v"(w[2])
-        : "v"(x), "v"(K[0]), "v"(K[1]), "v"(K[2]), "v"(K[3]), "v"(K[4]), "v"(K[5]), "v"(K[6]), "v"(K[7]), "v"(K[8]),
-          "v"(K[9]), "v"(K[10]), "v"(K[11]), "v"(K[12]), "v"(K[13]), "v"(K[14]));
-#undef W_L
-#else
-    for (int l = 0; l < 5; ++l) {
-        const double xl = dpp_row_bcast(x, l);
-        for (int r = 0; r < 3; ++r) w[r] = fma(xl, K[5 * r + l], w[r]);
-    }
+    acc = fma(dpp_row_bcast(src, 0), c0, acc);
+    acc = fma(dpp_row_bcast(src, 1), c1, acc);
 #endif
 }
 
 // LQ solve over the wave with zero initial state and homogeneous dynamics: stage linear terms at ogl -> odz
-// (the caller syncs before reading odz).  Backward: p_{k} = gx_k + A_k' p_{k+1} + K_k' h_k with h = gw + B' p
-// (lane i: p_i); the control right-hand sides h_k go to odz's w slots, and after the recursion every stage
-// forms its feed-forward kk_k = -(L D L')^-1 h_k at once (lane k); forward: w = kk + K x, x <- A x + B w
-// (lane i: x_i).  Each recursion loads stage k - 1's (k + 1's) data while it works on stage k, so a stage
-// waits on no LDS read: what remains on its chain are the broadcast FMAs.  oracle solve_core().
-struct SolBk { double B0[5], B1[5], Ac[5], Kc[3], h0, h1, h2, gx; };
-struct SolFw { double K[15], Ar[5], b0, b1, t[3]; };
-__device__ inline void sol_load_bk(const ldsd* L, const Layout& Y, int ogl, int k, int me, SolBk& R) {
+// (the caller syncs before reading odz).  Backward: p_{k} = gx_k + A_k' p_{k+1} + K_k' h_k with h = gw + B' p;
+// lane i holds p_i and, for i < 2, h_i (its own dot product with B's column i), which the co-state update
+// takes by broadcast; the control right-hand sides h_k go to odz's w slots, and after the recursion every
+// stage forms its feed-forward kk_k = -(L D L')^-1 h_k at once (lane k).  Forward: x <- A x + B w with
+// w = kk + K x; lane i holds x_i and, for i < 3, w_i (K's row i against x).  Each recursion loads stage k - 1's
+// (k + 1's) data while it works on stage k.  Every sum keeps oracle solve_core()'s terms and order.
+struct SolBk { double Br[5], Ac[5], Kc[3], h, h2, gx; };
+struct SolFw { double Kr[5], Ar[5], b0, b1, t; };
+__device__ inline void sol_load_bk(const ldsd* L, const Layout& Y, int ogl, int k, int me, int rh, SolBk& R) {
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
-        R.B0[l] = L[Y.oB + 10 * k + 2 * l];
-        R.B1[l] = L[Y.oB + 10 * k + 2 * l + 1];
+        R.Br[l] = L[Y.oB + 10 * k + 2 * l + rh];
         R.Ac[l] = L[Y.oA + 25 * k + 5 * l + me];
     }
 #pragma unroll
     for (int r = 0; r < 3; ++r) R.Kc[r] = L[Y.oK + 15 * k + 5 * r + me];
-    R.h0 = L[ogl + ZS * k + 5];
-    R.h1 = L[ogl + ZS * k + 6];
+    R.h = L[ogl + ZS * k + 5 + rh];
     R.h2 = L[ogl + ZS * k + 7];
     R.gx = L[ogl + ZS * k + me];
 }
-__device__ inline void sol_load_fw(const ldsd* L, const Layout& Y, int odz, int k, int me, SolFw& R) {
+__device__ inline void sol_load_fw(const ldsd* L, const Layout& Y, int odz, int k, int me, int rw, SolFw& R) {
 #pragma unroll
-    for (int i = 0; i < 15; ++i) R.K[i] = L[Y.oK + 15 * k + i];
-#pragma unroll
-    for (int l = 0; l < 5; ++l) R.Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
+    for (int l = 0; l < 5; ++l) {
+        R.Kr[l] = L[Y.oK + 15 * k + 5 * rw + l];
+        R.Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
+    }
     R.b0 = L[Y.oB + 10 * k + 2 * me];
     R.b1 = L[Y.oB + 10 * k + 2 * me + 1];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) R.t[r] = L[odz + ZS * k + 5 + r];
+    R.t = L[odz + ZS * k + 5 + rw];
 }
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
     if (REC_LANES(ln)) {
-        const int me = (ln & 15) < 5 ? (ln & 15) : 4;
+        const int me = (ln & 15) < 5 ? (ln & 15) : 4, rh = (ln & 15) < 2 ? (ln & 15) : 1;
         double p = (ln & 15) < 5 ? L[ogl + ZS * N + me] : 0.0;
         auto step = [&](const SolBk& c, int k) {
-            double h0 = c.h0, h1 = c.h1;
-            sol_h(h0, h1, p, c.B0, c.B1);
-            if (ln == 0) {
-                L[odz + ZS * k + 5] = h0;
-                L[odz + ZS * k + 6] = h1;
-                L[odz + ZS * k + 7] = c.h2;
-            }
+            double h = c.h;                       // h_rh = gw_rh + sum_l B(l, rh) p_l
+            dot5_lanes(h, p, c.Br);
+            if (ln < 2) L[odz + ZS * k + 5 + ln] = h;
+            if (ln == 2) L[odz + ZS * k + 7] = c.h2;
             double v = c.gx;
             dot5_lanes(v, p, c.Ac);
-            v = fma(c.Kc[0], h0, v);
-            v = fma(c.Kc[1], h1, v);
+            dot2_lanes(v, h, c.Kc[0], c.Kc[1]);   // + K(0, me) h_0 + K(1, me) h_1
             v = fma(c.Kc[2], c.h2, v);
             p = v;
         };
         // two stages per trip, alternating buffers: each stage's loads are in flight during the other's work
         SolBk ra, rb;
-        sol_load_bk(L, Y, ogl, N - 1, me, ra);
+        sol_load_bk(L, Y, ogl, N - 1, me, rh, ra);
         int k = N - 1;
         for (; k >= 1; k -= 2) {
-            sol_load_bk(L, Y, ogl, k - 1, me, rb);
+            sol_load_bk(L, Y, ogl, k - 1, me, rh, rb);
             step(ra, k);
-            sol_load_bk(L, Y, ogl, k >= 2 ? k - 2 : 0, me, ra);
+            sol_load_bk(L, Y, ogl, k >= 2 ? k - 2 : 0, me, rh, ra);
             step(rb, k - 1);
         }
         if (k == 0) step(ra, 0);
@@ -1164,32 +1128,29 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
     }
     sync();
     if (REC_LANES(ln)) {
-        const int me = (ln & 15) < 5 ? (ln & 15) : 4;
+        const int me = (ln & 15) < 5 ? (ln & 15) : 4, rw = (ln & 15) < 3 ? (ln & 15) : 2;
         double x = 0.0;
         auto step = [&](const SolFw& c, int k) {
-            double w[3] = {c.t[0], c.t[1], c.t[2]};
-            sol_w(w, x, c.K);
+            double w = c.t;                       // w_rw = kk_rw + sum_l K(rw, l) x_l
+            dot5_lanes(w, x, c.Kr);
             double xn = 0.0;
             dot5_lanes(xn, x, c.Ar);
-            xn = fma(c.b0, w[0], xn);
-            xn = fma(c.b1, w[1], xn);
-            // stage k overwritten after every lane has read its feed-forward terms (program order within the
+            dot2_lanes(xn, w, c.b0, c.b1);        // + B(me, 0) w_0 + B(me, 1) w_1
+            // stage k overwritten after every lane has read its feed-forward term (program order within the
             // wave; the emulation's broadcasts above are barriers)
             if (ln < 5) L[odz + ZS * k + ln] = x;
-            if (ln == 0)
-#pragma unroll
-                for (int r = 0; r < 3; ++r) L[odz + ZS * k + 5 + r] = w[r];
+            if (ln < 3) L[odz + ZS * k + 5 + ln] = w;
             x = xn;
         };
         // two stages per trip, alternating buffers; a stage's feed-forward slots are read before the stage
         // before it is overwritten (the loads are issued first)
         SolFw fa, fb;
-        sol_load_fw(L, Y, odz, 0, me, fa);
+        sol_load_fw(L, Y, odz, 0, me, rw, fa);
         int k = 0;
         for (; k + 1 < N; k += 2) {
-            sol_load_fw(L, Y, odz, k + 1, me, fb);
+            sol_load_fw(L, Y, odz, k + 1, me, rw, fb);
             step(fa, k);
-            sol_load_fw(L, Y, odz, k + 2 < N ? k + 2 : k + 1, me, fa);
+            sol_load_fw(L, Y, odz, k + 2 < N ? k + 2 : k + 1, me, rw, fa);
             step(fb, k + 1);
         }
         if (k < N) step(fa, k);
@@ -1353,7 +1314,8 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     solve_core(X, Y.oGL, Y.oDZ);
     sync();
     double n0 = 0.0, n1 = 0.0;
-    if (X.fin) {
+    const int fin = X.fin;
+    if (fin) {
         const double b0 = rE[0] - L[Y.oDZ + ZS * N + 0], b1 = rE[1] - L[Y.oDZ + ZS * N + 4];
         const double e0 = L[Y.oSC + SC_EM0], e1 = L[Y.oSC + SC_EM1], e2 = L[Y.oSC + SC_EM2], e3 = L[Y.oSC + SC_EM3];
         const double det = e0 * e3 - e1 * e2;
@@ -1363,11 +1325,11 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     X.nu[0] = n0;
     X.nu[1] = n1;
     sync();
-    if (X.fin)
+    if (fin)
         for (int k = X.ln; k <= N; k += WAVE)
 #pragma unroll
             for (int i = 0; i < NZ; ++i)
-                L[Y.oDZ + ZS * k + i] += X.nu[0] * L[Y.oEZ + 2 * ZS * k + i] + X.nu[1] * L[Y.oEZ + 2 * ZS * k + ZS + i];
+                L[Y.oDZ + ZS * k + i] += n0 * L[Y.oEZ + 2 * ZS * k + i] + n1 * L[Y.oEZ + 2 * ZS * k + ZS + i];
     sync();
 }
 
@@ -1399,16 +1361,16 @@ __device__ void rollout(const Ctx& X, int oz) {
 }
 
 // gradient of the QP objective 1/2 z'(H + delta I)z + gq'z at stage k
-__device__ void grad_f(const Ctx& X, int k, int oz, double g[NZ]) {
-    const int nv = k < X.N ? NZ : 5;
+__device__ __forceinline__ void grad_f(const ldsd* L, const Layout& Y, int N, double delta, int k, int oz, double g[NZ]) {
+    const int nv = k < N ? NZ : 5;
     double z[NZ], H[NH];
 #pragma unroll
-    for (int i = 0; i < NZ; ++i) z[i] = X.L[oz + ZS * k + i];
+    for (int i = 0; i < NZ; ++i) z[i] = L[oz + ZS * k + i];
 #pragma unroll
-    for (int i = 0; i < NH; ++i) H[i] = X.L[X.Y.oH + HSTR * k + i];
+    for (int i = 0; i < NH; ++i) H[i] = L[Y.oH + HSTR * k + i];
 #pragma unroll
     for (int i = 0; i < NZ; ++i) {
-        double v = X.L[X.Y.oGQ + ZS * k + i] + (i < nv ? X.delta * z[i] : 0.0);
+        double v = L[Y.oGQ + ZS * k + i] + (i < nv ? delta * z[i] : 0.0);
 #pragma unroll
         for (int j = 0; j < NZ; ++j) v += H[hidx(i, j)] * z[j];
         g[i] = i < nv ? v : 0.0;
@@ -1422,21 +1384,24 @@ __device__ int eqp(Ctx& X, double scale) {
     const int N = X.N;
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
+    const int fin_c = X.fin;
+    const double e0 = X.e[0], e1 = X.e[1];
     for (int k = X.ln; k <= N; k += WAVE)
 #pragma unroll
         for (int j = 0; j < NR; ++j) L[Y.oY + NR * k + j] = act_bit(X, Y.oTACT, k, j) ? L[Y.oTLAM + NR * k + j] : 0.0;
     sync();
     if (!factor_reg(X, 1)) return -1;
+    const double delta = X.delta;
     rollout(X, Y.oTZ);
     for (int it = 0; it < AL_STEPS; ++it) {
         for (int k = X.ln; k <= N; k += WAVE) {
             double g[NZ], z[NZ];
-            grad_f(X, k, Y.oTZ, g);
+            grad_f(L, Y, N, delta, k, Y.oTZ, g);
 #pragma unroll
             for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
             const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
             const unsigned act = (unsigned)L[Y.oTACT + k];
-            for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+            for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
                 const bool use = on && ((act >> j) & 1u);
                 const RowSp r = row_sp(kind, k < N, kb, vb);
                 const double f = RHO * sp_dot(r, L[Y.oG + NR * k + j], z) - L[Y.oY + NR * k + j];
@@ -1451,7 +1416,7 @@ __device__ int eqp(Ctx& X, double scale) {
             for (int u = 0; u < NZ; ++u) L[Y.oGL + ZS * k + u] = g[u];
         }
         sync();
-        const double rE[2] = {X.e[0] - L[Y.oTZ + ZS * N + 0], X.e[1] - L[Y.oTZ + ZS * N + 4]};
+        const double rE[2] = {e0 - L[Y.oTZ + ZS * N + 0], e1 - L[Y.oTZ + ZS * N + 4]};
         solve(X, rE);
         double upd = 0.0, ym = 0.0;
         for (int k = X.ln; k <= N; k += WAVE) {
@@ -1462,7 +1427,7 @@ __device__ int eqp(Ctx& X, double scale) {
             for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
             const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
             const unsigned act = (unsigned)L[Y.oTACT + k];
-            for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+            for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
                 const bool use = on && ((act >> j) & 1u);
                 const double d = RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
                 const double y = L[Y.oY + NR * k + j] - d;
@@ -1488,7 +1453,7 @@ __device__ int eqp(Ctx& X, double scale) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+        for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
             const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
             const double y = L[Y.oY + NR * k + j];
             const bool in = (mask >> j) & 1u;
@@ -1515,6 +1480,9 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
     const int nq = (N + 1) * NR, nzq = (N + 1) * ZS;      // row slots, stage-variable slots
+    // the context's scalars the iterations read, taken once (the context lives in private memory)
+    const int dbg = X.dbg, fin_c = X.fin, max_iter = X.P.max_iter;
+    const double tol = X.P.tol, e0 = X.e[0], e1 = X.e[1];
     if (!resume) rollout(X, Y.oZ);
     int m = 0;
     for (int k = X.ln; k <= N; k += WAVE) {
@@ -1522,7 +1490,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+        for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
             if (!resume) {
                 const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
                 if (on) {
@@ -1537,11 +1505,11 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     sync();
     double phi = resume ? *phi_io : 1.0;
     int it = resume ? *iters : 0, rc = 1;
-    for (; it < X.P.max_iter; ++it) {
+    for (; it < max_iter; ++it) {
         double mu = 0.0;
         PhOpen(ph_red, X, PH_IRED);
         for (int k = X.ln; k <= N; k += WAVE) {
-            const int nr = stage_nrows(k, N, X.fin);
+            const int nr = stage_nrows(k, N, fin_c);
 #pragma unroll
             for (int j = 0; j < NR; ++j) {      // every slot, the stage's rows applied (see for_rows)
                 const double t = mu + L[Y.oS + NR * k + j] * L[Y.oLAM + NR * k + j];
@@ -1551,26 +1519,27 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         mu = wsum(mu) / m;
         PhClose(ph_red);
         if (!isfinite(mu)) { rc = -1; break; }
-        if (mu <= X.P.tol && phi <= 1e-12) { rc = 0; break; }
+        if (mu <= tol && phi <= 1e-12) { rc = 0; break; }
         if (!resume && mu <= MU_CHECK && phi <= MU_CHECK) {
             double tie = 0.0;
             for (int q = X.ln; q < nq; q += WAVE) {
-                const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                 const double sv = L[Y.oS + q], lv = L[Y.oLAM + q];
                 if (r.on && !(sv > CHECK_SEP * lv || lv > CHECK_SEP * sv)) tie = 1.0;
             }
             if (wmax(tie) == 0.0) { rc = 2; break; }
         }
-        if (X.dbg & 1) (void)factor_reg(X, 0);
+        if (dbg & 1) (void)factor_reg(X, 0);
         if (!factor_reg(X, 0)) { rc = -1; break; }
-        const double rE[2] = {X.e[0] - L[Y.oZ + ZS * N + 0], X.e[1] - L[Y.oZ + ZS * N + 4]};
+        const double delta = X.delta;
+        const double rE[2] = {e0 - L[Y.oZ + ZS * N + 0], e1 - L[Y.oZ + ZS * N + 4]};
         for (int pass = 0; pass < 2; ++pass) {
             double sigma_mu = 0.0;
             if (pass == 1) {
                 PhOpen(ph_r1, X, PH_IRED);
                 double am = 1.0;
                 for (int q = X.ln; q < nq; q += WAVE) {
-                    const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                    const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                     const double dsa = L[Y.oDSA + q], dla = L[Y.oDLA + q];
                     const double rs = -L[Y.oS + q] / dsa, rl = -L[Y.oLAM + q] / dla;
                     am = (r.on && dsa < 0.0) ? fmin(am, rs) : am;
@@ -1579,7 +1548,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 am = wmin(am);
                 double mua = 0.0;
                 for (int k = X.ln; k <= N; k += WAVE) {
-                    const int nr = stage_nrows(k, N, X.fin);
+                    const int nr = stage_nrows(k, N, fin_c);
 #pragma unroll
                     for (int j = 0; j < NR; ++j) {
                         const double t = mua + (L[Y.oS + NR * k + j] + am * L[Y.oDSA + NR * k + j]) *
@@ -1593,11 +1562,11 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 PhClose(ph_r1);
             }
             PhOpen(ph_g, X, PH_IGRAD);
-            for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 2) & 1); ++rp_) {
+            for (int rp_ = 0; rp_ < 1 + ((dbg >> 2) & 1); ++rp_) {
                 // each row's f = l + (rs - l rp) / s, row-parallel, into DS (free until this pass's
                 // direction rows write it); then each stage folds its rows into the gradient in row order
                 for (int q = X.ln; q < nq; q += WAVE) {
-                    const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                    const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                     const double s = L[Y.oS + q], l = L[Y.oLAM + q];
                     double rs = -s * l;
                     if (pass == 1) rs += sigma_mu - L[Y.oDSA + q] * L[Y.oDLA + q];
@@ -1611,9 +1580,9 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 sync();
                 for (int k = X.ln; k <= N; k += WAVE) {
                     double g[NZ];
-                    grad_f(X, k, Y.oZ, g);
+                    grad_f(L, Y, N, delta, k, Y.oZ, g);
                     const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-                    for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+                    for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
                         const RowSp r = row_sp(kind, k < N, kb, vb);
                         const double f = L[Y.oDS + NR * k + j];
                         const double g0 = g[r.i0] - f * r.c0;
@@ -1630,13 +1599,13 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             }
             sync();
             PhClose(ph_g);
-            if (X.dbg & 2) solve(X, rE);
+            if (dbg & 2) solve(X, rE);
             solve(X, rE);
             const int ods = pass == 0 ? Y.oDSA : Y.oDS, odl = pass == 0 ? Y.oDLA : Y.oDL;
             PhOpen(ph_d, X, PH_IDIR);
-            for (int rp_ = 0; rp_ < 1 + ((X.dbg >> 3) & 1); ++rp_)
+            for (int rp_ = 0; rp_ < 1 + ((dbg >> 3) & 1); ++rp_)
             for (int q = X.ln; q < nq; q += WAVE) {
-                const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+                const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                 const double s = L[Y.oS + q], l = L[Y.oLAM + q];
                 double rs = -s * l;
                 if (pass == 1) rs += sigma_mu - L[Y.oDSA + q] * L[Y.oDLA + q];
@@ -1660,7 +1629,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         PhOpen(ph_r2, X, PH_IRED);
         double amax = 1.0 / TAU, fin = 1.0;
         for (int q = X.ln; q < nq; q += WAVE) {
-            const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+            const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
             const double ds = L[Y.oDS + q], dl = L[Y.oDL + q];
             const double rs = -L[Y.oS + q] / ds, rl = -L[Y.oLAM + q] / dl;
             amax = (r.on && ds < 0.0) ? fmin(amax, rs) : amax;
@@ -1675,7 +1644,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         for (int q = X.ln; q < nzq; q += WAVE)
             if (q % ZS < NZ) L[Y.oZ + q] += alpha * L[Y.oDZ + q];
         for (int q = X.ln; q < nq; q += WAVE) {
-            const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+            const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
             const double sn = L[Y.oS + q] + alpha * L[Y.oDS + q];
             const double ln_ = L[Y.oLAM + q] + alpha * L[Y.oDL + q];
             if (r.on) {
@@ -1799,7 +1768,7 @@ __device__ void multipliers(Ctx& X) {
     // stage gradients of the Lagrangian minus the rows (x part) into GL; lateral multipliers
     for (int k = X.ln; k <= N; k += WAVE) {
         double g[NZ];
-        grad_f(X, k, Y.oZ, g);
+        grad_f(L, Y, N, X.delta, k, Y.oZ, g);
         L[Y.oMLAT + 2 * k] = 0.0;
         L[Y.oMLAT + 2 * k + 1] = 0.0;
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
