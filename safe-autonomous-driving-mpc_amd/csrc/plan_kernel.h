@@ -1209,10 +1209,8 @@ __device__ bool factor_par(const Ctx& X) {
             for (int u = 0; u < 8; ++u) R.m[u] = ht(k, u);
             R.h77 = L[oHS + 8 * k + 7];
         };
-        auto step = [&](const FacIn& c, int k) -> bool {
-            double m[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) m[u] = c.m[u];
+        auto step = [&](FacIn& c, int k) -> bool {
+            double* m = c.m;                  // M's column, formed in place over HT's (no register copies)
             double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
             fac_pab(q, Pc, c.abc);
             fac_m(m, c.abc, q);
@@ -1239,9 +1237,8 @@ __device__ bool factor_par(const Ctx& X) {
 #pragma unroll
                 for (int i = 0; i < 6; ++i) L[oL + 6 * k + i] = Lc[i];
             if (k > 0) {
-                double pn[5] = {m[0], m[1], m[2], m[3], m[4]};
-                fac_pn(pn, m[5], m[6], m[7], kc);
-                fac_sym(Pc, pn, sel);
+                fac_pn(m, m[5], m[6], m[7], kc);    // Pn's column over M_xx's, in place
+                fac_sym(Pc, m, sel);
             }
             return true;
         };

@@ -183,18 +183,23 @@ class Planner:
         i32 = dict(dtype=torch.int32, device=dev)
         d_st = torch.as_tensor(starts, **f64).contiguous()
         d_avg = torch.as_tensor(np.ascontiguousarray(avg, np.float64), **f64).contiguous()
-        out = dict(X=torch.zeros((B, Cn, Nmax + 1, 5), **f64), U=torch.zeros((B, Cn, Nmax, 2), **f64),
-                   S=torch.zeros((B, Cn, Nmax), **f64))
+        # every slot a plan uses is written by the kernel (slots past nchunks[b] are never read): no fill
+        out = dict(X=torch.empty((B, Cn, Nmax + 1, 5), **f64), U=torch.empty((B, Cn, Nmax, 2), **f64),
+                   S=torch.empty((B, Cn, Nmax), **f64))
         for k in ("N", "is_final", "status", "iters", "sqp"):
-            out[k] = torch.zeros((B, Cn), **i32)
-        out["nchunks"] = torch.zeros(B, **i32)
+            out[k] = torch.empty((B, Cn), **i32)
+        out["nchunks"] = torch.empty(B, **i32)
         stream = torch.cuda.current_stream(dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
         _check(lib().plan_optimize_device(self.h, B, int(Nmax), d_st.data_ptr(), float(max_chunk_size), Cn,
                                           d_avg.data_ptr(), int(d_avg.numel()),
                                           *[out[k].data_ptr() for k in ("X", "U", "S", "N", "is_final", "status",
                                                                         "iters", "sqp", "nchunks")],
                                           C.c_void_p(stream.cuda_stream)), "plan_optimize_device")
+        ev[1].record(stream)
         torch.cuda.synchronize(dev)
+        self.last_kernel_s = ev[0].elapsed_time(ev[1]) / 1e3
         return {k: v.cpu().numpy() for k, v in out.items()}
 
     def route_eval(self, s):

@@ -293,14 +293,21 @@ def _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, stat
     def loop(act, Nm):
         """loop launches sized for Nm over the plans act"""
         while act.size:
-            C_ = int(min(seg, max_chunks - used[act].min()))
+            # slots per plan: enough for the longest remaining distance at about half a chunk committed per
+            # intermediate chunk (plans that use them all continue in the next launch)
+            est = int(np.ceil(float(np.max(s_total - cur[act, 0])) / (0.5 * max_chunk_size))) + 4
+            C_ = int(min(seg, est, max_chunks - used[act].min()))
             if C_ <= 0:
                 break
+            # longest remaining distance first: a launch lasts as long as its slowest wavefront's chain, and
+            # with more plans than resident slots the plans dispatched last start late (results are per plan)
+            act = act[np.argsort(-(s_total - cur[act, 0]), kind="stable")]
             t0 = time.perf_counter()
             r = pl.optimize_device(cur[act], max_chunk_size, C_, avg, Nm, device=device)
             if timing is not None:
                 timing.setdefault("launches", []).append({"kind": "loop", "Nmax": int(Nm), "plans": int(act.size),
-                                                          "slots": C_, "seconds": time.perf_counter() - t0})
+                                                          "slots": C_, "seconds": time.perf_counter() - t0,
+                                                          "kernel_seconds": pl.last_kernel_s})
             nxt = []
             for i, b in enumerate(act):
                 nc = int(r["nchunks"][i])

@@ -1,5 +1,5 @@
-"""Fleet leg breakdown (bench.plan_fleet): the device chunk loop's launches per tier, the host assembly and
-checks; then the same with one tier (the launch sized for the longest final chunk) for comparison.
+"""Fleet leg breakdown (bench.plan_fleet): the device chunk loop's launches, the host assembly and checks;
+with the plans dispatched longest remaining distance first, then in index order for comparison.
 usage: python tools/fleet_probe.py [B]"""
 import json
 import os
@@ -14,8 +14,10 @@ import bench  # noqa: E402
 import mpcplan  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-for label in ("two tiers", "one tier"):
-    if label == "one tier":
-        mpcplan.Planner.chunks_per_cu = lambda self, n: 1
+import numpy as np  # noqa: E402
+for label in ("longest first", "index order"):
+    if label == "index order":
+        _argsort = np.argsort
+        np.argsort = lambda a, kind=None: _argsort(np.zeros_like(a), kind="stable")
     f = bench.plan_fleet(B, 0)
     print(label, json.dumps({k: f[k] for k in ("seconds", "chunks", "checks_passed", "breakdown")}), flush=True)
