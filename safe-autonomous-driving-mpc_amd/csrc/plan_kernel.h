@@ -1594,7 +1594,6 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 }
                 sync();
             }
-            sync();
             PhClose(ph_g);
             if (dbg & 2) solve(X, rE);
             solve(X, rE);
