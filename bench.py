@@ -656,7 +656,7 @@ def plan_fleet(B, device):
             "breakdown": {"launches": [{k: (round(v, 4) if isinstance(v, float) else v) for k, v in l.items()}
                                        for l in tm.get("launches", [])],
                           "loop_seconds": tm["loop_seconds"], "checks_seconds": tm["seconds"] - tm["loop_seconds"],
-                          "note": "launches: plan_optimize_device calls (launch, run, copy back; kernel_seconds: HIP events around the kernel); "
+                          "note": "launches: plan_optimize calls (upload, kernel, download); "
                                   "checks: plan assembly and the restated checks on every plan"},
             "round_loop": {"seconds": dt_r, "plans_per_s": B / dt_r, "identical_plans": bool(same),
                            "note": "one batched chunk launch per round from the host (device_loop=False): each "

@@ -131,6 +131,13 @@ int plan_optimize_device(plan_ctx* c, int B, int Nmax, const double* starts, dou
                          const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final,
                          int* status, int* iters, int* sqp, int* nchunks, void* stream);
 
+/* plan_optimize_device with host buffers, synchronous (inputs staged, outputs copied back): the same
+ * arguments and outputs, slot = b * max_chunks + n.  Lets a host caller run the device chunk loop without a
+ * device allocator of its own. */
+int plan_optimize(plan_ctx* c, int B, int Nmax, const double* starts, double max_chunk_size, int max_chunks,
+                  const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final, int* status,
+                  int* iters, int* sqp, int* nchunks);
+
 /* Route functions on the device, for tests: kappa(s) and dkappa/ds (k_ref_fun, :445-459), v_max(s). */
 int plan_route_eval(plan_ctx* c, int n, const double* s, double* kappa, double* dkappa, double* vmax);
 

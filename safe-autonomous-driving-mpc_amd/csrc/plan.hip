@@ -362,6 +362,60 @@ int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const 
     return PLAN_SUCCESS;
 }
 
+int plan_optimize(plan_ctx* c, int B, int Nmax, const double* starts, double max_chunk_size, int max_chunks,
+                  const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final, int* status,
+                  int* iters, int* sqp, int* nchunks) {
+    if (!c) return fail(PLAN_E_ARG, "ctx is NULL");
+    if (B < 0) return fail(PLAN_E_ARG, "B must be >= 0");
+    if (B == 0) return PLAN_SUCCESS;
+    if (!starts || !avg || !X || !U || !S || !N || !is_final || !status || !iters || !sqp || !nchunks)
+        return fail(PLAN_E_ARG, "plan_optimize: every array is required");
+    if (Nmax < 1 || Nmax > PLAN_MAX_N) return fail(PLAN_E_ARG, "Nmax out of range [1, PLAN_MAX_N]");
+    if (max_chunks < 1) return fail(PLAN_E_ARG, "max_chunks must be >= 1");
+    if (nav < 1) return fail(PLAN_E_ARG, "avg must have at least one entry");
+    if (hipSetDevice(c->device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");
+    const size_t slots = (size_t)B * max_chunks;
+    const size_t nX = slots * (Nmax + 1) * 5, nU = slots * Nmax * 2, nS = slots * Nmax;
+    const size_t bytes = sizeof(double) * (5 * (size_t)B + nav + nX + nU + nS) + sizeof(int) * (5 * slots + B);
+    if (bytes > c->io_bytes) {
+        if (c->io) (void)hipFree(c->io);
+        c->io = nullptr;
+        c->io_bytes = 0;
+        if (hipMalloc(&c->io, bytes) != hipSuccess) return fail(PLAN_E_ALLOC, "staging allocation failed");
+        c->io_bytes = bytes;
+    }
+    double* d_st = (double*)c->io;
+    double* d_avg = d_st + 5 * (size_t)B;
+    double* d_X = d_avg + nav;
+    double* d_U = d_X + nX;
+    double* d_S = d_U + nU;
+    int* d_N = (int*)(d_S + nS);
+    int* d_fin = d_N + slots;
+    int* d_status = d_fin + slots;
+    int* d_iters = d_status + slots;
+    int* d_sqp = d_iters + slots;
+    int* d_nch = d_sqp + slots;
+    if (hipMemcpy(d_st, starts, sizeof(double) * 5 * B, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_avg, avg, sizeof(double) * nav, hipMemcpyHostToDevice) != hipSuccess)
+        return fail(PLAN_E_DEVICE, "input upload failed");
+    int rc = plan_optimize_device(c, B, Nmax, d_st, max_chunk_size, max_chunks, d_avg, nav, d_X, d_U, d_S, d_N,
+                                  d_fin, d_status, d_iters, d_sqp, d_nch, nullptr);
+    if (rc != PLAN_SUCCESS) return rc;
+    if (hipError_t e = hipDeviceSynchronize(); e != hipSuccess)
+        return fail(PLAN_E_DEVICE, std::string("plan loop kernel failed: ") + hipGetErrorString(e));
+    const bool ok = hipMemcpy(X, d_X, sizeof(double) * nX, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(U, d_U, sizeof(double) * nU, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(S, d_S, sizeof(double) * nS, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(N, d_N, sizeof(int) * slots, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(is_final, d_fin, sizeof(int) * slots, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(status, d_status, sizeof(int) * slots, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(iters, d_iters, sizeof(int) * slots, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(sqp, d_sqp, sizeof(int) * slots, hipMemcpyDeviceToHost) == hipSuccess &&
+                    hipMemcpy(nchunks, d_nch, sizeof(int) * B, hipMemcpyDeviceToHost) == hipSuccess;
+    if (!ok) return fail(PLAN_E_DEVICE, "output download failed");
+    return PLAN_SUCCESS;
+}
+
 int plan_route_eval(plan_ctx* c, int n, const double* s, double* kappa, double* dkappa, double* vmax) {
     if (!c) return fail(PLAN_E_ARG, "ctx is NULL");
     if (n < 0 || (n > 0 && (!s || !kappa || !dkappa || !vmax))) return fail(PLAN_E_ARG, "bad arguments");

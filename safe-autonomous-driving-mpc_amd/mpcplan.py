@@ -33,7 +33,7 @@ class PlanError(RuntimeError):
 
 
 EXPORTS = ["plan_default_params", "plan_create", "plan_solve_chunks", "plan_solve_chunks_device", "plan_optimize_device",
-           "plan_route_eval", "plan_chunks_per_cu", "plan_set_params", "plan_last_error", "plan_version", "plan_destroy"]
+           "plan_optimize", "plan_route_eval", "plan_chunks_per_cu", "plan_set_params", "plan_last_error", "plan_version", "plan_destroy"]
 
 _lib = None
 
@@ -56,6 +56,9 @@ def lib():
     L.plan_optimize_device.restype = C.c_int
     L.plan_optimize_device.argtypes = ([C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_double, C.c_int, C.c_void_p,
                                         C.c_int] + [C.c_void_p] * 10)
+    L.plan_optimize.restype = C.c_int
+    L.plan_optimize.argtypes = ([C.c_void_p, C.c_int, C.c_int, _dp, C.c_double, C.c_int, _dp, C.c_int] + [_dp] * 3 +
+                                [_ip] * 6)
     L.plan_route_eval.restype = C.c_int
     L.plan_route_eval.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp]
     L.plan_chunks_per_cu.restype = C.c_int
@@ -170,37 +173,24 @@ class Planner:
                 groups.append((n, n))
         return groups
 
-    def optimize_device(self, starts, max_chunk_size, max_chunks, avg, Nmax, device=0):
-        """plan_optimize_device (include/mpcplan.h): the chunk loop of optimize_full_trajectory for B plans on
-        the device, up to max_chunks chunks each.  starts [B,5]; avg [nav] = mean(vmax[i:]).  Returns dict of
-        numpy arrays: X [B,C,Nmax+1,5], U [B,C,Nmax,2], S [B,C,Nmax], N, is_final, status, iters, sqp [B,C]
-        (C = max_chunks slots) and nchunks [B]."""
-        import torch
-        dev = torch.device("cuda", device)
+    def optimize_device(self, starts, max_chunk_size, max_chunks, avg, Nmax, device=None):
+        """The chunk loop of optimize_full_trajectory for B plans on the device (plan_optimize: host buffers,
+        the kernel is plan_optimize_device's), up to max_chunks chunks each.  starts [B,5]; avg [nav] =
+        mean(vmax[i:]).  Returns dict of numpy arrays: X [B,C,Nmax+1,5], U [B,C,Nmax,2], S [B,C,Nmax], N,
+        is_final, status, iters, sqp [B,C] (C = max_chunks slots; slots past nchunks[b] are not written) and
+        nchunks [B].  Needs no torch (device: the context's; the argument is kept for callers)."""
         starts = np.ascontiguousarray(starts, np.float64).reshape(-1, 5)
-        B, Cn = starts.shape[0], int(max_chunks)
-        f64 = dict(dtype=torch.float64, device=dev)
-        i32 = dict(dtype=torch.int32, device=dev)
-        d_st = torch.as_tensor(starts, **f64).contiguous()
-        d_avg = torch.as_tensor(np.ascontiguousarray(avg, np.float64), **f64).contiguous()
-        # every slot a plan uses is written by the kernel (slots past nchunks[b] are never read): no fill
-        out = dict(X=torch.empty((B, Cn, Nmax + 1, 5), **f64), U=torch.empty((B, Cn, Nmax, 2), **f64),
-                   S=torch.empty((B, Cn, Nmax), **f64))
+        avg = np.ascontiguousarray(avg, np.float64)
+        B, Cn, Nm = starts.shape[0], int(max_chunks), int(Nmax)
+        out = dict(X=np.empty((B, Cn, Nm + 1, 5)), U=np.empty((B, Cn, Nm, 2)), S=np.empty((B, Cn, Nm)))
         for k in ("N", "is_final", "status", "iters", "sqp"):
-            out[k] = torch.empty((B, Cn), **i32)
-        out["nchunks"] = torch.empty(B, **i32)
-        stream = torch.cuda.current_stream(dev)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record(stream)
-        _check(lib().plan_optimize_device(self.h, B, int(Nmax), d_st.data_ptr(), float(max_chunk_size), Cn,
-                                          d_avg.data_ptr(), int(d_avg.numel()),
-                                          *[out[k].data_ptr() for k in ("X", "U", "S", "N", "is_final", "status",
-                                                                        "iters", "sqp", "nchunks")],
-                                          C.c_void_p(stream.cuda_stream)), "plan_optimize_device")
-        ev[1].record(stream)
-        torch.cuda.synchronize(dev)
-        self.last_kernel_s = ev[0].elapsed_time(ev[1]) / 1e3
-        return {k: v.cpu().numpy() for k, v in out.items()}
+            out[k] = np.empty((B, Cn), np.int32)
+        out["nchunks"] = np.empty(B, np.int32)
+        _check(lib().plan_optimize(self.h, B, Nm, _p(starts), float(max_chunk_size), Cn, _p(avg), int(avg.size),
+                                   *[_p(out[k]) for k in ("X", "U", "S")],
+                                   *[_pi(out[k]) for k in ("N", "is_final", "status", "iters", "sqp", "nchunks")]),
+               "plan_optimize")
+        return out
 
     def route_eval(self, s):
         """kappa(s), d kappa / ds and v_max(s) on the device (k_ref_fun / v_max_fun)."""

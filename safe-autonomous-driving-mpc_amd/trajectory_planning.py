@@ -306,8 +306,7 @@ def _device_loop(route, starts, max_chunk_size, max_chunks, device, pieces, stat
             r = pl.optimize_device(cur[act], max_chunk_size, C_, avg, Nm, device=device)
             if timing is not None:
                 timing.setdefault("launches", []).append({"kind": "loop", "Nmax": int(Nm), "plans": int(act.size),
-                                                          "slots": C_, "seconds": time.perf_counter() - t0,
-                                                          "kernel_seconds": pl.last_kernel_s})
+                                                          "slots": C_, "seconds": time.perf_counter() - t0})
             nxt = []
             for i, b in enumerate(act):
                 nc = int(r["nchunks"][i])

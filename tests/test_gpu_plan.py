@@ -9,8 +9,12 @@ the chunks (measured 0.996-1.000), and both sides converge on >= 95% of the chun
 (the oracle's PLAN_QP_FAILED: e.g. 15 of the 256 traj1 N = 10 chunks start with a curvature outside the
 k bounds that 3 s cannot undo, or must stop within the horizon).
 """
+import os
+
 import numpy as np
 import pytest
+
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -315,3 +319,24 @@ def test_residency_groups(env):
             assert np.array_equal(one["X"], g["X"][sl, :n + 1]) and np.array_equal(one["status"], g["status"][sl])
     print(f"\nchunks per CU by Nmax: {dict(zip(range(1, 65), occ))}; groups of {hs}: {groups}")
     pl.close()
+
+
+def test_device_loop_needs_no_torch(env):
+    """The device chunk loop (plan_optimize, host buffers) runs in a fresh process that never imports torch:
+    the planner's HIP runtime is the only one initialised there, and the plans equal the round loop's."""
+    import subprocess
+    import sys
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path[:0] = [{os.path.join(ROOT, 'safe-autonomous-driving-mpc_amd')!r}, {ROOT!r}]\n"
+        "import workloads as W, trajectory_planning as TP\n"
+        "r = W.plan_route('traj1')\n"
+        "starts = np.zeros((4, 5)); starts[1:, 0] = [40.0, 120.0, 200.0]; starts[1:, 4] = 5.0\n"
+        "pd, sd = TP.optimize_full_trajectory_batch(r, starts)\n"
+        "ph, sh = TP.optimize_full_trajectory_batch(r, starts, device_loop=False)\n"
+        "assert all(np.array_equal(a[0], b[0]) for a, b in zip(pd, ph))\n"
+        "assert 'torch' not in sys.modules, 'torch was imported'\n"
+        "print('ok', [len(q['statuses']) for q in sd])\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert out.stdout.startswith("ok")

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(built):
     out = subprocess.run(["nm", "-D", "--defined-only", built], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r"\sT\s+(plan_[a-z_]+)$", out, flags=re.M))
     names = declared_functions()
-    assert len(names) == 11 and not [n for n in names if n not in exported]
+    assert len(names) == 12 and not [n for n in names if n not in exported]
     import mpcplan
     assert sorted(mpcplan.EXPORTS) == names
 
