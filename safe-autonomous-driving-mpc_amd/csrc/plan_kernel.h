@@ -27,7 +27,7 @@ constexpr int NH = 36;            // packed symmetric 8x8
 // stage-parallel loop (lane k on stage k) spread over the LDS banks (a stride of 8 doubles = 16 dwords put
 // every fourth lane on the same bank group: SQ_LDS_BANK_CONFLICT was 39% of the LDS-active cycles)
 constexpr int ZS = NZ + 1;
-constexpr int HSTR = NH + 1;
+constexpr int HSTR = NH + 9;     // a stage's H block: packed H (36), the factorisation's 8 slots (hs_slot), 1 / HT(7, 7)
 constexpr double RHO = 1e8;       // penalty of the active rows in the equality-constrained solve
 constexpr int AL_STEPS = 4;
 constexpr double AL_TOL = 1e-13;   // refinements stop once the multiplier update is at rounding level
@@ -79,7 +79,7 @@ inline void route_grid(const double* s, int M, int T, int* grid, double* ginv) {
 // point alias the polish's: DSA = Y, DLA = TLAM, DS = TZ (the polish runs after the interior point is done).
 struct Layout {
     int NP;
-    int oA, oB, oC, oH, oHS, oGQ, oG, oK, oL, oEZ, oZ, oS, oLAM, oGL, oDZ, oDSA, oDLA, oDS, oDL, oMY, oMLAT, oZB,
+    int oAB, oH, oGQ, oG, oK, oL, oEZ, oZ, oS, oLAM, oGL, oDZ, oDSA, oDLA, oDS, oDL, oMY, oMLAT, oZB,
         oZ2, oDZV, oPI, oVLIM, oVL, oACT, oTACT, oSC, oWK;
     int oY, oTLAM, oTZ;
     int total;
@@ -90,12 +90,11 @@ __host__ __device__ Layout make_layout(int Nmax) {
     y.NP = Nmax + 1;
     int o = 0;
     const int np = y.NP;
-    y.oA = o; o += 25 * np;
-    y.oB = o; o += 10 * np;          // u1, u2 columns (the slack's column is zero)
-    y.oC = o; o += 5 * np;
-    y.oH = o; o += HSTR * np;
-    y.oHS = o; o += 8 * np;          // the factorisation's stage Hessian H + delta I + row weights at the 8
-                                     // entries rows touch (hs_slot); elsewhere it is H + delta I
+    y.oAB = o; o += 40 * np;         // the dynamics [A B c] by rows (ab_at): A(l, j) at 8 l + j, B(l, r) (u1, u2;
+                                     // the slack's column is zero) at 8 l + 5 + r, c(l) at 8 l + 7
+    y.oH = o; o += HSTR * np;        // packed H, then at NH + slot the factorisation's stage Hessian H + delta I +
+                                     // row weights at the 8 entries rows touch (hs_slot; elsewhere it is H + delta I), then
+                                     // 1 / HT(7, 7)
     y.oGQ = o; o += ZS * np;
     y.oG = o; o += NR * np;
     y.oK = o; o += 15 * np;
@@ -526,6 +525,9 @@ __host__ __device__ constexpr int hx(int i, int j) {   // packed index of the sy
     return i * NZ - (i * (i - 1)) / 2 + (j - i);
 }
 __device__ inline int hidx(int i, int j) { return i <= j ? hx(i, j) : hx(j, i); }
+// [A B c] of stage k, row l, column c (0..4 A, 5..6 B, 7 c): one stride per stage and per row, so a lane that
+// reads a column (or a row) adds one offset per stage and takes the rest as immediate offsets
+__host__ __device__ constexpr int ab_at(int k, int l, int c) { return 40 * k + 8 * l + c; }
 
 // the 8 entries of a stage Hessian the rows touch, slots 0..7: (0,0) terminal row; (3,3), (3,4), (4,4) curvature
 // and lateral rows; (4,7) and (7,7) speed and slack rows (with (4,4)); (5,5), (6,6) control boxes
@@ -720,11 +722,9 @@ __device__ void interval_hess_fold(Ctx& X, int k, const double xa[5], const doub
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
 #pragma unroll
-        for (int j = 0; j < 5; ++j) T[i][j] = L[Y.oA + 25 * k + 5 * i + j];
-        T[i][5] = L[Y.oB + 10 * k + 2 * i];
-        T[i][6] = L[Y.oB + 10 * k + 2 * i + 1];
+        for (int j = 0; j < 7; ++j) T[i][j] = L[Y.oAB + ab_at(k, i, j)];
         T[i][7] = 0.0;
-        c[i] = L[Y.oC + 5 * k + i];
+        c[i] = L[Y.oAB + ab_at(k, i, 7)];
     }
     double HbT[5][NZ], HabT[5][NZ];
 #pragma unroll
@@ -809,13 +809,9 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
                 ok = false;
             } else {
 #pragma unroll
-                for (int i = 0; i < 5; ++i) {
+                for (int i = 0; i < 5; ++i)
 #pragma unroll
-                    for (int j = 0; j < 5; ++j) L[Y.oA + 25 * k + 5 * i + j] = R[8 * i + j];
-                    L[Y.oB + 10 * k + 2 * i] = R[8 * i + 5];
-                    L[Y.oB + 10 * k + 2 * i + 1] = R[8 * i + 6];
-                    L[Y.oC + 5 * k + i] = R[8 * i + 7];
-                }
+                    for (int j = 0; j < 8; ++j) L[Y.oAB + ab_at(k, i, j)] = R[8 * i + j];   // R's rows are [A B c]
                 if (exact) {
                     double y[5];
 #pragma unroll
@@ -911,7 +907,7 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
                 H[c] = use ? hc : H[c];
             }
         });
-        ldsd* hs = L + Y.oHS + 8 * k;
+        ldsd* hs = L + Y.oH + HSTR * k + NH;
         hs[0] = H[hx(0, 0)];
         hs[1] = H[hx(3, 3)];
         hs[2] = H[hx(3, 4)];
@@ -920,6 +916,7 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
         hs[5] = H[hx(5, 5)];
         hs[6] = H[hx(6, 6)];
         hs[7] = H[hx(7, 7)];
+        hs[8] = 1.0 / H[hx(7, 7)];          // the third pivot's reciprocal, formed here stage-parallel (factor_par)
     }
 }
 
@@ -1065,8 +1062,8 @@ struct SolFw { double Kr[5], Ar[5], b0, b1, t; };
 __device__ inline void sol_load_bk(const ldsd* L, const Layout& Y, int ogl, int k, int me, int rh, SolBk& R) {
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
-        R.Br[l] = L[Y.oB + 10 * k + 2 * l + rh];
-        R.Ac[l] = L[Y.oA + 25 * k + 5 * l + me];
+        R.Br[l] = L[Y.oAB + ab_at(k, l, 5 + rh)];
+        R.Ac[l] = L[Y.oAB + ab_at(k, l, me)];
     }
 #pragma unroll
     for (int r = 0; r < 3; ++r) R.Kc[r] = L[Y.oK + 15 * k + 5 * r + me];
@@ -1078,10 +1075,10 @@ __device__ inline void sol_load_fw(const ldsd* L, const Layout& Y, int odz, int 
 #pragma unroll
     for (int l = 0; l < 5; ++l) {
         R.Kr[l] = L[Y.oK + 15 * k + 5 * rw + l];
-        R.Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
+        R.Ar[l] = L[Y.oAB + ab_at(k, me, l)];
     }
-    R.b0 = L[Y.oB + 10 * k + 2 * me];
-    R.b1 = L[Y.oB + 10 * k + 2 * me + 1];
+    R.b0 = L[Y.oAB + ab_at(k, me, 5)];
+    R.b1 = L[Y.oAB + ab_at(k, me, 6)];
     R.t = L[odz + ZS * k + 5 + rw];
 }
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
@@ -1175,18 +1172,24 @@ __device__ bool factor_par(const Ctx& X) {
     const int N = X.N, ln = X.ln;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
-    const int oA = UNI(Y.oA), oB = UNI(Y.oB), oH = UNI(Y.oH), oHS = UNI(Y.oHS), oK = UNI(Y.oK), oL = UNI(Y.oL);
+    const int oAB = UNI(Y.oAB), oH = UNI(Y.oH), oK = UNI(Y.oK), oL = UNI(Y.oL);
     const double delta = X.delta;
-    double okv = 1.0;
+    int okw = 1;
     if (REC_LANES(ln)) {
         const int j = (ln & 15) < 7 ? (ln & 15) : 7;
-        // HT(u, j) of stage k: the HS slot or the packed H entry (a per-lane base and stride, no branch); dg:
-        // the diagonal entries H + delta I adds to
-        auto ht = [&](int k, int u) {
+        // HT(u, j) of stage k: the slot or the packed H entry, at a per-lane offset in the stage's H block (no
+        // select per stage); the non-slot diagonal entries (1, 1), (2, 2) add delta (ht_at: h + delta there):
+        // v + dg1 with dg1 = delta on lane 1 and +0 elsewhere is fma(j == 1, delta, v) bit for bit
+        int hoff[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
             const int sl = hs_slot(u, j);
-            const double v = L[sl >= 0 ? oHS + sl + 8 * k : oH + hidx(u, j) + HSTR * k];
-            // ht_at: (u == w && u < nv) ? h + delta : h for the non-slot diagonal entries (1, 1), (2, 2)
-            return u == 1 ? fma(j == 1 ? 1.0 : 0.0, delta, v) : (u == 2 ? fma(j == 2 ? 1.0 : 0.0, delta, v) : v);
+            hoff[u] = sl >= 0 ? NH + sl : hidx(u, j);
+        }
+        const double dg1 = j == 1 ? delta : 0.0, dg2 = j == 2 ? delta : 0.0;
+        auto ht = [&](int k, int u) {
+            const double v = L[oH + HSTR * k + hoff[u]];
+            return u == 1 ? v + dg1 : (u == 2 ? v + dg2 : v);
         };
         double Pc[5], sel[5];
 #pragma unroll
@@ -1194,22 +1197,21 @@ __device__ bool factor_par(const Ctx& X) {
             Pc[i] = ht(N, i);
             sel[i] = (j == i) ? 0.5 : 0.0;
         }
-        // column j of [A B] (lane 7: zeros), read at a per-lane base and strides
-        const int abase = j < 5 ? oA + j : (j < 7 ? oB + (j - 5) : oA), akst = j < 5 ? 25 : 10, alst = j < 5 ? 5 : 2;
-        const bool aon = j < 7;
+        // column j of [A B c] (lanes 7..15: the c column, whose values no other lane reads), one stage offset
+        const int abase = oAB + j;
         // one stage's inputs: column j of [A B], of HT (with delta) and HT(7, 7)
-        struct FacIn { double abc[5], m[8], h77; };
+        struct FacIn { double abc[5], m[8], h77, r77; };
         auto load = [&](int k, FacIn& R) {
 #pragma unroll
-            for (int l = 0; l < 5; ++l) {
-                const double v = L[abase + akst * k + alst * l];
-                R.abc[l] = aon ? v : 0.0;
-            }
+            for (int l = 0; l < 5; ++l) R.abc[l] = L[abase + ab_at(k, l, 0)];
 #pragma unroll
             for (int u = 0; u < 8; ++u) R.m[u] = ht(k, u);
-            R.h77 = L[oHS + 8 * k + 7];
+            R.h77 = L[oH + HSTR * k + NH + 7];
+            R.r77 = L[oH + HSTR * k + NH + 8];
         };
-        auto step = [&](FacIn& c, int k) -> bool {
+        // one stage; false (uniform: every operand of a pivot is a broadcast or a uniform load) when a pivot is not
+        // positive, after which the stage's stores are garbage the caller never reads
+        auto step = [&](FacIn& c, int k) -> int {
             double* m = c.m;                  // M's column, formed in place over HT's (no register copies)
             double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
             fac_pab(q, Pc, c.abc);
@@ -1218,16 +1220,14 @@ __device__ bool factor_par(const Ctx& X) {
             fac_mww(t, m[5], m[6]);
             // chol3 of [[M55, ., .], [M65, M66, .], [0, 0, HT77]] (oracle chol3, same operations)
             const double d0 = t[0];
-            if (!(d0 > 0.0)) return false;
             Lc[0] = 1.0 / d0;
             Lc[1] = t[1] * Lc[0];
             const double d1 = t[2] - Lc[1] * t[1];
-            if (!(d1 > 0.0)) return false;
             Lc[2] = 1.0 / d1;
             Lc[3] = 0.0;
             Lc[4] = 0.0;
-            if (!(c.h77 > 0.0)) return false;
-            Lc[5] = 1.0 / c.h77;
+            Lc[5] = c.r77;                    // 1.0 / HT(7, 7), from stage_hess_par
+            const int ok = d0 > 0.0 && d1 > 0.0 && c.h77 > 0.0;
             double kc[3] = {-m[5], -m[6], -m[7]};
             chol3_solve(Lc, kc);
             if (ln < 5)
@@ -1240,21 +1240,24 @@ __device__ bool factor_par(const Ctx& X) {
                 fac_pn(m, m[5], m[6], m[7], kc);    // Pn's column over M_xx's, in place
                 fac_sym(Pc, m, sel);
             }
-            return true;
+            return ok;
         };
-        // two stages per trip, alternating buffers: a stage's inputs are in flight during the other's work
+        // two stages per trip, alternating buffers: a stage's inputs are in flight during the other's work; the
+        // pivot test is a scalar branch
         FacIn fa, fb;
         load(N - 1, fa);
         int k = N - 1;
         for (; k >= 1; k -= 2) {
             load(k - 1, fb);
-            if (!step(fa, k)) { okv = 0.0; break; }
+            okw = UNI(step(fa, k));
+            if (!okw) break;
             load(k >= 2 ? k - 2 : 0, fa);
-            if (!step(fb, k - 1)) { okv = 0.0; break; }
+            okw = UNI(step(fb, k - 1));
+            if (!okw) break;
         }
-        if (okv != 0.0 && k == 0 && !step(fa, 0)) okv = 0.0;
+        if (okw && k == 0) okw = UNI(step(fa, 0));
     }
-    if (wmin(okv) == 0.0) return false;
+    if (!okw) return false;
     sync();
     if (X.fin) {
         for (int c = 0; c < 2; ++c) {
@@ -1348,8 +1351,8 @@ __device__ void rollout(const Ctx& X, int oz) {
             if (k == N) break;
             double Ar[5];
 #pragma unroll
-            for (int l = 0; l < 5; ++l) Ar[l] = L[Y.oA + 25 * k + 5 * me + l];
-            double v = L[Y.oC + 5 * k + me];
+            for (int l = 0; l < 5; ++l) Ar[l] = L[Y.oAB + ab_at(k, me, l)];
+            double v = L[Y.oAB + ab_at(k, me, 7)];
             dot5_lanes(v, x, Ar);
             x = v;
         }
@@ -1794,7 +1797,7 @@ __device__ void multipliers(Ctx& X) {
             if (k > 0) {
                 double Ac[5];
 #pragma unroll
-                for (int l = 0; l < 5; ++l) Ac[l] = L[Y.oA + 25 * k + 5 * l + me];
+                for (int l = 0; l < 5; ++l) Ac[l] = L[Y.oAB + ab_at(k, l, me)];
                 double v = L[Y.oGL + ZS * k + me];
                 dot5_lanes(v, pi, Ac);
                 pi = v;
