@@ -772,7 +772,8 @@ __device__ void interval_hess_fold(Ctx& X, int k, const double xa[5], const doub
 // the QP at the SQP iterate in ZB (stage-parallel); returns false (uniform) when a defect Jacobian is singular
 __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
     PHASE(PH_BUILD);
-    const int N = X.N;
+    const int N = UNI(X.N);
+    const int fin_u = UNI(X.fin);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const plan_params& P = X.P;
@@ -820,11 +821,11 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
                 }
             }
         }
-        const int nr = stage_nrows(k, N, X.fin);
+        const int nr = stage_nrows(k, N, fin_u);
         const double kk = x[3], v = x[4];
         for (int j = 0; j < nr; ++j) {
             double gv = 0.0;
-            switch (row_kind(k, X.N, X.fin, j)) {
+            switch (row_kind(k, N, fin_u, j)) {
                 case ROW_VMIN: gv = v + sl - P.v_min; break;
                 case ROW_VMAX: gv = (frozen ? L[Y.oVLIM + k] : route_vmax(X.R, x[0])) - (v + sl); break;
                 case ROW_LATP: gv = P.a_max - kk * v * v; break;
@@ -840,7 +841,7 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
             }
             L[Y.oG + NR * k + j] = gv;
         }
-        if (exact && k > 0 && !(X.fin && k == N)) {
+        if (exact && k > 0 && !(fin_u && k == N)) {
             const double lp = L[Y.oMLAT + 2 * k], lm = L[Y.oMLAT + 2 * k + 1];
             L[Y.oH + HSTR * k + hx(3, 4)] += 2.0 * v * (lp - lm);
             L[Y.oH + HSTR * k + hx(4, 4)] += 2.0 * kk * (lp - lm);
@@ -860,14 +861,15 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
 // (interior point), 1: RHO on the TACT rows (polish)
 __device__ void stage_hess_par(Ctx& X, int mode) {
     PHASE(PH_HESS);
-    const int N = X.N;
+    const int N = UNI(X.N);
+    const int fin_u = UNI(X.fin);
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
     if (mode == 0) {
         // the barrier weights w = lam / s, row-parallel, into DS (free at the top of an interior-point
         // iteration: the previous step has been taken)
         for (int q = X.ln; q < (N + 1) * NR; q += WAVE) {
-            const RowAt r = row_at(L, Y.oZB, q, N, X.fin);
+            const RowAt r = row_at(L, Y.oZB, q, N, fin_u);
             const double w = L[Y.oLAM + q] / L[Y.oS + q];
             if (r.on) L[Y.oDS + q] = w;
         }
@@ -893,7 +895,7 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
             if (i < nv) H[hx(i, i)] += X.delta;
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         const unsigned act = mode == 0 ? 0u : (unsigned)L[Y.oTACT + k];
-        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+        for_rows(k, N, fin_u, [&](int kind, int j, bool on) {
             const double w = mode == 0 ? L[Y.oDS + NR * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
             const bool use = on && w != 0.0;
             const RowSp r = row_sp(kind, k < N, kb, vb);
@@ -1082,7 +1084,7 @@ __device__ inline void sol_load_fw(const ldsd* L, const Layout& Y, int odz, int 
     R.t = L[odz + ZS * k + 5 + rw];
 }
 __device__ void solve_core(const Ctx& X, int ogl, int odz) {
-    const int N = X.N, ln = X.ln;
+    const int N = UNI(X.N), ln = X.ln;
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
     if (REC_LANES(ln)) {
@@ -1169,7 +1171,7 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
 // matrix.  Column j of HT comes from the packed H (+ delta on the diagonal) except at the 8 entries rows
 // touch, which stage_hess_par stored in HS (ht_at).
 __device__ bool factor_par(const Ctx& X) {
-    const int N = X.N, ln = X.ln;
+    const int N = UNI(X.N), ln = X.ln;
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const int oAB = UNI(Y.oAB), oH = UNI(Y.oH), oK = UNI(Y.oK), oL = UNI(Y.oL);
@@ -1310,11 +1312,11 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     PROF_COUNT(PH_NSOLVE);
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
-    const int N = X.N;
+    const int N = UNI(X.N);
     solve_core(X, Y.oGL, Y.oDZ);
     sync();
     double n0 = 0.0, n1 = 0.0;
-    const int fin = X.fin;
+    const int fin = UNI(X.fin);
     if (fin) {
         const double b0 = rE[0] - L[Y.oDZ + ZS * N + 0], b1 = rE[1] - L[Y.oDZ + ZS * N + 4];
         const double e0 = L[Y.oSC + SC_EM0], e1 = L[Y.oSC + SC_EM1], e2 = L[Y.oSC + SC_EM2], e3 = L[Y.oSC + SC_EM3];
@@ -1337,7 +1339,7 @@ __device__ void solve(Ctx& X, const double rE[2]) {
 // rollout())
 __device__ void rollout(const Ctx& X, int oz) {
     PHASE(PH_ROLLOUT);
-    const int N = X.N, ln = X.ln;
+    const int N = UNI(X.N), ln = X.ln;
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
     if (REC_LANES(ln)) {
@@ -1381,10 +1383,10 @@ __device__ __forceinline__ void grad_f(const ldsd* L, const Layout& Y, int N, do
 // > 0 = offending rows (flipped in TACT), -1 = breakdown (uniform)
 __device__ int eqp(Ctx& X, double scale) {
     PHASE(PH_EQP);
-    const int N = X.N;
+    const int N = UNI(X.N);
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
-    const int fin_c = X.fin;
+    const int fin_c = UNI(X.fin);
     const double e0 = X.e[0], e1 = X.e[1];
     for (int k = X.ln; k <= N; k += WAVE)
 #pragma unroll
@@ -1476,12 +1478,12 @@ __device__ int eqp(Ctx& X, double scale) {
 // continues from Z, S, LAM, *iters, *phi_io (oracle ipm)
 __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     PHASE(PH_IPM);
-    const int N = X.N;
+    const int N = UNI(X.N);
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
     const int nq = (N + 1) * NR, nzq = (N + 1) * ZS;      // row slots, stage-variable slots
     // the context's scalars the iterations read, taken once (the context lives in private memory)
-    const int dbg = X.dbg, fin_c = X.fin, max_iter = X.P.max_iter;
+    const int dbg = UNI(X.dbg), fin_c = UNI(X.fin), max_iter = UNI(X.P.max_iter);
     const double tol = X.P.tol, e0 = X.e[0], e1 = X.e[1];
     if (!resume) rollout(X, Y.oZ);
     int m = 0;
@@ -1687,12 +1689,13 @@ __device__ double ipm_mask(const Ctx& X, int k) {
 
 // one QP: 0 solved (KKT point), 1 interior-point answer without a certified polish, -1 failure (uniform)
 __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
-    const int N = X.N;
+    const int N = UNI(X.N);
+    const int fin_u = UNI(X.fin);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     double scale = 1.0;
     for (int k = X.ln; k <= N; k += WAVE) {
-        const int nr = stage_nrows(k, N, X.fin);
+        const int nr = stage_nrows(k, N, fin_u);
 #pragma unroll
         for (int j = 0; j < NR; ++j) scale = j < nr ? fmax(scale, fabs(L[Y.oG + NR * k + j])) : scale;
     }
@@ -1761,7 +1764,8 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
 // NLP multipliers from the QP solution (oracle multipliers()): MY, MLAT
 __device__ void multipliers(Ctx& X) {
     PHASE(PH_MULT);
-    const int N = X.N;
+    const int N = UNI(X.N);
+    const int fin_u = UNI(X.fin);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     // stage gradients of the Lagrangian minus the rows (x part) into GL; lateral multipliers
@@ -1771,7 +1775,7 @@ __device__ void multipliers(Ctx& X) {
         L[Y.oMLAT + 2 * k] = 0.0;
         L[Y.oMLAT + 2 * k + 1] = 0.0;
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
-        for_rows(k, N, X.fin, [&](int kind, int j, bool on) {
+        for_rows(k, N, fin_u, [&](int kind, int j, bool on) {
             const RowSp r = row_sp(kind, k < N, kb, vb);
             const double l = L[Y.oLAM + NR * k + j];
             const double g0 = g[r.i0] - l * r.c0;
@@ -1791,7 +1795,7 @@ __device__ void multipliers(Ctx& X) {
     if (REC_LANES(X.ln)) {
         const int ln = X.ln, me = (ln & 15) < 5 ? (ln & 15) : 4;
         double pi = L[Y.oGL + ZS * N + me];
-        if (X.fin) pi += me == 0 ? X.nu[0] : (me == 4 ? X.nu[1] : 0.0);
+        if (fin_u) pi += me == 0 ? X.nu[0] : (me == 4 ? X.nu[1] : 0.0);
         for (int k = N - 1; k >= 0; --k) {
             if (ln < 5) L[Y.oPI + 5 * k + ln] = pi;
             if (k > 0) {
@@ -1829,7 +1833,7 @@ __device__ void multipliers(Ctx& X) {
 // the NLP's cost (:128-170) and L1 violation at ZB + alpha * DZV (stage-parallel, reduced)
 __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
     PHASE(PH_LSEARCH);
-    const int N = X.N;
+    const int N = UNI(X.N);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const plan_params& P = X.P;
@@ -1876,7 +1880,7 @@ __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
 
 __device__ double cost_dir(const Ctx& X) {
     PHASE(PH_LSEARCH);
-    const int N = X.N;
+    const int N = UNI(X.N);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const plan_params& P = X.P;
@@ -1895,7 +1899,7 @@ __device__ inline ldsd* lds_p(const Ctx& X) { return X.L; }
 // one chunk NLP (trajectory_planning.py:351-390) at X.x0, X.st, X.fin, X.N, set by the caller: the plan is
 // left in the LDS block (ZB); returns the status, the interior-point iterations and QPs in *total_out, *nq_out
 __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) {
-    const int N = X.N;
+    const int N = UNI(X.N);
     X.den = fmax(1.0, X.R.s_total - X.x0[0]);
     X.nu[0] = X.nu[1] = 0.0;
     X.delta = 0.0;
@@ -2064,7 +2068,7 @@ __global__ void __launch_bounds__(WAVE) plan_chunk_kernel(KArgs a) {
         }
         return;
     }
-    const int N = X.N;
+    const int N = UNI(X.N);
     X.fin = a.fin ? (a.fin[b] != 0) : 0;
 #pragma unroll
     for (int i = 0; i < 5; ++i) X.x0[i] = a.x0[5 * (size_t)b + i];
@@ -2166,7 +2170,7 @@ __global__ void __launch_bounds__(WAVE) plan_loop_kernel(LArgs a) {
         X.st = x0[0] + size;
         int total = 0, nq = 0;
         const int status = solve_chunk(X, &total, &nq);
-        const int N = X.N;
+        const int N = UNI(X.N);
         const size_t slot = (size_t)b * a.max_chunks + n;
         ldsd* L = X.L;
         for (int k = X.ln; k <= Nm; k += WAVE) {
