@@ -350,10 +350,10 @@ __device__ void defect(const DevRoute& R, const plan_params& P, const double xa[
 // stage; (k > 0) curvature min, max; (k < N) u1 min, max, u2 min, max, slack; the intermediate chunk's
 // terminal row at k = N.  Counted and indexed arithmetically (no per-lane array, which would live in
 // scratch memory).
-__device__ inline int stage_nrows(int k, int N, int fin) {
+__host__ __device__ constexpr int stage_nrows(int k, int N, int fin) {
     return ((fin && k == N) ? 0 : (k > 0 ? 4 : 2)) + (k > 0 ? 2 : 0) + (k < N ? 5 : 0) + ((k == N && !fin) ? 1 : 0);
 }
-__device__ inline int row_kind(int k, int N, int fin, int j) {
+__host__ __device__ constexpr int row_kind(int k, int N, int fin, int j) {
     const int n0 = (fin && k == N) ? 0 : (k > 0 ? 4 : 2);
     if (j < n0) return j;                                   // ROW_VMIN, ROW_VMAX, ROW_LATP, ROW_LATM
     j -= n0;
@@ -436,16 +436,24 @@ struct RowAt {
     bool on, two;
     double c0, c1;
 };
+// the kinds of a stage's slots 0..10, 4 bits per slot (slots past the stage's rows: ROW_STERM), for the four
+// stage shapes: first stage (k = 0 < N), interior, last stage of the final chunk, last stage of an intermediate
+// chunk -- row_kind tabulated, so a slot's kind is a shift of a selected constant instead of a select chain
+__host__ __device__ constexpr unsigned long long kind_tab(int k, int N, int fin) {
+    unsigned long long t = 0;
+    for (int j = 0; j < NR; ++j)
+        t |= (unsigned long long)(j < stage_nrows(k, N, fin) ? row_kind(k, N, fin, j) : ROW_STERM) << (4 * j);
+    return t;
+}
+constexpr unsigned long long KIND_FIRST = kind_tab(0, 2, 0), KIND_MID = kind_tab(1, 2, 0), KIND_LASTF = kind_tab(2, 2, 1),
+                             KIND_LASTI = kind_tab(2, 2, 0);
 __device__ inline RowAt row_at(const ldsd* L, int oZB, int q, int N, int fin) {
     RowAt r;
     const int k = q / NR, j = q - NR * k;
     r.k = k;
-    const int n0 = (fin && k == N) ? 0 : (k > 0 ? 4 : 2);
-    const int n1 = k > 0 ? 2 : 0;
-    const int n2 = k < N ? 5 : 0;
-    const int n3 = (k == N && !fin) ? 1 : 0;
-    r.on = j < n0 + n1 + n2 + n3;
-    const int kind = j < n0 ? j : (j < n0 + n1 ? ROW_KMIN + (j - n0) : (j < n0 + n1 + n2 ? ROW_U1MIN + (j - n0 - n1) : ROW_STERM));
+    r.on = j < stage_nrows(k, N, fin);
+    const unsigned long long tab = k == N ? (fin ? KIND_LASTF : KIND_LASTI) : (k == 0 ? KIND_FIRST : KIND_MID);
+    const int kind = (int)((tab >> (4 * j)) & 15ull);
     // nibble tables over the kinds (ROW_VMIN .. ROW_STERM): first and second coefficient's variable
     constexpr unsigned long long I0TAB = 0x076655333344ull;   // kind 0..11: 4 4 3 3 3 3 5 5 6 6 7 0
     constexpr unsigned long long I1TAB = 0x076655334477ull;   // kind 0..11: 7 7 4 4 3 3 5 5 6 6 7 0
@@ -771,6 +779,7 @@ __device__ void interval_hess_fold(Ctx& X, int k, const double xa[5], const doub
 
 // the QP at the SQP iterate in ZB (stage-parallel); returns false (uniform) when a defect Jacobian is singular
 __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     PHASE(PH_BUILD);
     const int N = UNI(X.N);
     const int fin_u = UNI(X.fin);
@@ -779,7 +788,7 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
     const plan_params& P = X.P;
     const double den = X.den;
     bool ok = true;
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
         double x[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) x[i] = L[Y.oZB + ZS * k + i];
@@ -860,6 +869,7 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
 // the factorisation's stage Hessians HT = H + delta I + sum w a a' (stage-parallel); mode 0: w = lam / s
 // (interior point), 1: RHO on the TACT rows (polish)
 __device__ void stage_hess_par(Ctx& X, int mode) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     PHASE(PH_HESS);
     const int N = UNI(X.N);
     const int fin_u = UNI(X.fin);
@@ -868,14 +878,14 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
     if (mode == 0) {
         // the barrier weights w = lam / s, row-parallel, into DS (free at the top of an interior-point
         // iteration: the previous step has been taken)
-        for (int q = X.ln; q < (N + 1) * NR; q += WAVE) {
+        for (int q = ln; q < (N + 1) * NR; q += WAVE) {
             const RowAt r = row_at(L, Y.oZB, q, N, fin_u);
             const double w = L[Y.oLAM + q] / L[Y.oS + q];
             if (r.on) L[Y.oDS + q] = w;
         }
         sync();
     }
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
         // only the 8 entries rows touch are stored (hs_slot); the rest of the factorisation Hessian is
         // H + delta I, formed where it is read (ht_at)
         double H[NH];
@@ -1308,6 +1318,7 @@ __device__ bool factor_reg(Ctx& X, int mode) {
 
 // full solve (GL filled and synced): DZ; meets E dz_N = rE exactly (final chunk); X.nu = terminal forces
 __device__ void solve(Ctx& X, const double rE[2]) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     PHASE(PH_SOLVE);
     PROF_COUNT(PH_NSOLVE);
     ldsd* L = X.L;
@@ -1328,7 +1339,7 @@ __device__ void solve(Ctx& X, const double rE[2]) {
     X.nu[1] = n1;
     sync();
     if (fin)
-        for (int k = X.ln; k <= N; k += WAVE)
+        for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
             for (int i = 0; i < NZ; ++i)
                 L[Y.oDZ + ZS * k + i] += n0 * L[Y.oEZ + 2 * ZS * k + i] + n1 * L[Y.oEZ + 2 * ZS * k + ZS + i];
@@ -1382,13 +1393,14 @@ __device__ __forceinline__ void grad_f(const ldsd* L, const Layout& Y, int N, do
 // equality-constrained QP on the TACT rows (estimates TLAM), solution into TZ / TLAM; 0 = KKT-consistent,
 // > 0 = offending rows (flipped in TACT), -1 = breakdown (uniform)
 __device__ int eqp(Ctx& X, double scale) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     PHASE(PH_EQP);
     const int N = UNI(X.N);
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
     const int fin_c = UNI(X.fin);
     const double e0 = X.e[0], e1 = X.e[1];
-    for (int k = X.ln; k <= N; k += WAVE)
+    for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
         for (int j = 0; j < NR; ++j) L[Y.oY + NR * k + j] = act_bit(X, Y.oTACT, k, j) ? L[Y.oTLAM + NR * k + j] : 0.0;
     sync();
@@ -1396,7 +1408,7 @@ __device__ int eqp(Ctx& X, double scale) {
     const double delta = X.delta;
     rollout(X, Y.oTZ);
     for (int it = 0; it < AL_STEPS; ++it) {
-        for (int k = X.ln; k <= N; k += WAVE) {
+        for (int k = ln; k <= N; k += WAVE) {
             double g[NZ], z[NZ];
             grad_f(L, Y, N, delta, k, Y.oTZ, g);
 #pragma unroll
@@ -1421,7 +1433,7 @@ __device__ int eqp(Ctx& X, double scale) {
         const double rE[2] = {e0 - L[Y.oTZ + ZS * N + 0], e1 - L[Y.oTZ + ZS * N + 4]};
         solve(X, rE);
         double upd = 0.0, ym = 0.0;
-        for (int k = X.ln; k <= N; k += WAVE) {
+        for (int k = ln; k <= N; k += WAVE) {
 #pragma unroll
             for (int u = 0; u < NZ; ++u) L[Y.oTZ + ZS * k + u] += L[Y.oDZ + ZS * k + u];
             double z[NZ];
@@ -1447,7 +1459,7 @@ __device__ int eqp(Ctx& X, double scale) {
     double fin = 1.0;
     int bad = 0;
     const double tr = 1e-9 * scale, tl = 1e-9 * scale;
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) fin = isfinite(L[Y.oTZ + ZS * k + u]) ? fin : 0.0;
         unsigned mask = (unsigned)L[Y.oTACT + k];
@@ -1477,6 +1489,7 @@ __device__ int eqp(Ctx& X, double scale) {
 // checkpoint (first call only: mu and phi below MU_CHECK, every row's s and lambda CHECK_SEP apart); resume
 // continues from Z, S, LAM, *iters, *phi_io (oracle ipm)
 __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     PHASE(PH_IPM);
     const int N = UNI(X.N);
     ldsd* L = X.L;
@@ -1487,7 +1500,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     const double tol = X.P.tol, e0 = X.e[0], e1 = X.e[1];
     if (!resume) rollout(X, Y.oZ);
     int m = 0;
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
         double z[NZ];
 #pragma unroll
         for (int u = 0; u < NZ; ++u) z[u] = L[Y.oZ + ZS * k + u];
@@ -1510,7 +1523,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     for (; it < max_iter; ++it) {
         double mu = 0.0;
         PhOpen(ph_red, X, PH_IRED);
-        for (int k = X.ln; k <= N; k += WAVE) {
+        for (int k = ln; k <= N; k += WAVE) {
             const int nr = stage_nrows(k, N, fin_c);
 #pragma unroll
             for (int j = 0; j < NR; ++j) {      // every slot, the stage's rows applied (see for_rows)
@@ -1524,7 +1537,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         if (mu <= tol && phi <= 1e-12) { rc = 0; break; }
         if (!resume && mu <= MU_CHECK && phi <= MU_CHECK) {
             double tie = 0.0;
-            for (int q = X.ln; q < nq; q += WAVE) {
+            for (int q = ln; q < nq; q += WAVE) {
                 const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                 const double sv = L[Y.oS + q], lv = L[Y.oLAM + q];
                 if (r.on && !(sv > CHECK_SEP * lv || lv > CHECK_SEP * sv)) tie = 1.0;
@@ -1540,7 +1553,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             if (pass == 1) {
                 PhOpen(ph_r1, X, PH_IRED);
                 double am = 1.0;
-                for (int q = X.ln; q < nq; q += WAVE) {
+                for (int q = ln; q < nq; q += WAVE) {
                     const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                     const double dsa = L[Y.oDSA + q], dla = L[Y.oDLA + q];
                     const double rs = -L[Y.oS + q] / dsa, rl = -L[Y.oLAM + q] / dla;
@@ -1549,7 +1562,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 }
                 am = wmin(am);
                 double mua = 0.0;
-                for (int k = X.ln; k <= N; k += WAVE) {
+                for (int k = ln; k <= N; k += WAVE) {
                     const int nr = stage_nrows(k, N, fin_c);
 #pragma unroll
                     for (int j = 0; j < NR; ++j) {
@@ -1567,7 +1580,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             for (int rp_ = 0; rp_ < 1 + ((dbg >> 2) & 1); ++rp_) {
                 // each row's f = l + (rs - l rp) / s, row-parallel, into DS (free until this pass's
                 // direction rows write it); then each stage folds its rows into the gradient in row order
-                for (int q = X.ln; q < nq; q += WAVE) {
+                for (int q = ln; q < nq; q += WAVE) {
                     const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                     const double s = L[Y.oS + q], l = L[Y.oLAM + q];
                     double rs = -s * l;
@@ -1580,7 +1593,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                     if (r.on) L[Y.oDS + q] = f;
                 }
                 sync();
-                for (int k = X.ln; k <= N; k += WAVE) {
+                for (int k = ln; k <= N; k += WAVE) {
                     double g[NZ];
                     grad_f(L, Y, N, delta, k, Y.oZ, g);
                     const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
@@ -1605,7 +1618,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
             const int ods = pass == 0 ? Y.oDSA : Y.oDS, odl = pass == 0 ? Y.oDLA : Y.oDL;
             PhOpen(ph_d, X, PH_IDIR);
             for (int rp_ = 0; rp_ < 1 + ((dbg >> 3) & 1); ++rp_)
-            for (int q = X.ln; q < nq; q += WAVE) {
+            for (int q = ln; q < nq; q += WAVE) {
                 const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
                 const double s = L[Y.oS + q], l = L[Y.oLAM + q];
                 double rs = -s * l;
@@ -1629,22 +1642,22 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         }
         PhOpen(ph_r2, X, PH_IRED);
         double amax = 1.0 / TAU, fin = 1.0;
-        for (int q = X.ln; q < nq; q += WAVE) {
+        for (int q = ln; q < nq; q += WAVE) {
             const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
             const double ds = L[Y.oDS + q], dl = L[Y.oDL + q];
             const double rs = -L[Y.oS + q] / ds, rl = -L[Y.oLAM + q] / dl;
             amax = (r.on && ds < 0.0) ? fmin(amax, rs) : amax;
             amax = (r.on && dl < 0.0) ? fmin(amax, rl) : amax;
         }
-        for (int q = X.ln; q < nzq; q += WAVE)
+        for (int q = ln; q < nzq; q += WAVE)
             if (q % ZS < NZ) fin = isfinite(L[Y.oDZ + q]) ? fin : 0.0;
         amax = wmin(amax);
         fin = wmin(fin);
         const double alpha = fmin(1.0, TAU * amax);
         if (!isfinite(alpha) || fin == 0.0) { rc = -1; break; }
-        for (int q = X.ln; q < nzq; q += WAVE)
+        for (int q = ln; q < nzq; q += WAVE)
             if (q % ZS < NZ) L[Y.oZ + q] += alpha * L[Y.oDZ + q];
-        for (int q = X.ln; q < nq; q += WAVE) {
+        for (int q = ln; q < nq; q += WAVE) {
             const RowAt r = row_at(L, Y.oZB, q, N, fin_c);
             const double sn = L[Y.oS + q] + alpha * L[Y.oDS + q];
             const double ln_ = L[Y.oLAM + q] + alpha * L[Y.oDL + q];
@@ -1665,9 +1678,10 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
 
 // copy the polish result (TZ, TLAM, TACT) to the solution (Z, LAM, ACT)
 __device__ void accept_polish(const Ctx& X, bool with_act) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     ldsd* L = X.L;
     const Layout& Y = X.Y;
-    for (int k = X.ln; k <= X.N; k += WAVE) {
+    for (int k = ln; k <= X.N; k += WAVE) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) L[Y.oZ + ZS * k + u] = L[Y.oTZ + ZS * k + u];
 #pragma unroll
@@ -1689,12 +1703,13 @@ __device__ double ipm_mask(const Ctx& X, int k) {
 
 // one QP: 0 solved (KKT point), 1 interior-point answer without a certified polish, -1 failure (uniform)
 __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     const int N = UNI(X.N);
     const int fin_u = UNI(X.fin);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     double scale = 1.0;
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
         const int nr = stage_nrows(k, N, fin_u);
 #pragma unroll
         for (int j = 0; j < NR; ++j) scale = j < nr ? fmax(scale, fabs(L[Y.oG + NR * k + j])) : scale;
@@ -1702,7 +1717,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
     scale = wmax(scale);
     *iters = 0;
     if (have_cls) {
-        for (int k = X.ln; k <= N; k += WAVE) {
+        for (int k = ln; k <= N; k += WAVE) {
             L[Y.oTACT + k] = L[Y.oACT + k];
 #pragma unroll
             for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
@@ -1722,7 +1737,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
     if (rc == 2) {
         // checkpoint (oracle qp_solve): polish from the loose interior point's classification; the interior
         // point resumes where it stopped if that does not certify
-        for (int k = X.ln; k <= N; k += WAVE) {
+        for (int k = ln; k <= N; k += WAVE) {
             L[Y.oTACT + k] = ipm_mask(X, k);
 #pragma unroll
             for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
@@ -1740,7 +1755,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
     }
     if (rc < 0) return -1;
     const double nu_ipm[2] = {X.nu[0], X.nu[1]};
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
         L[Y.oTACT + k] = ipm_mask(X, k);
 #pragma unroll
         for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
@@ -1754,7 +1769,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
             return 0;
         }
     }
-    for (int k = X.ln; k <= N; k += WAVE) L[Y.oACT + k] = ipm_mask(X, k);
+    for (int k = ln; k <= N; k += WAVE) L[Y.oACT + k] = ipm_mask(X, k);
     sync();
     X.nu[0] = nu_ipm[0];
     X.nu[1] = nu_ipm[1];
@@ -1832,6 +1847,7 @@ __device__ void multipliers(Ctx& X) {
 
 // the NLP's cost (:128-170) and L1 violation at ZB + alpha * DZV (stage-parallel, reduced)
 __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     PHASE(PH_LSEARCH);
     const int N = UNI(X.N);
     ldsd* L = X.L;
@@ -1839,9 +1855,9 @@ __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
     const plan_params& P = X.P;
     auto zv = [&](int k, int i) { return L[Y.oZB + ZS * k + i] + (alpha != 0.0 ? alpha * L[Y.oDZV + ZS * k + i] : 0.0); };
     double c = 0.0, v = 0.0;
-    if (X.ln == 0)
+    if (ln == 0)
         for (int i = 0; i < 5; ++i) v += fabs(zv(0, i) - X.x0[i]);
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
         double x[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) x[i] = zv(k, i);
@@ -1879,13 +1895,14 @@ __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
 }
 
 __device__ double cost_dir(const Ctx& X) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     PHASE(PH_LSEARCH);
     const int N = UNI(X.N);
     ldsd* L = X.L;
     const Layout& Y = X.Y;
     const plan_params& P = X.P;
     double v = 0.0;
-    for (int k = X.ln; k < N; k += WAVE) {
+    for (int k = ln; k < N; k += WAVE) {
         v += 2.0 * P.w_y * (L[Y.oZB + ZS * k + 1] * L[Y.oDZV + ZS * k + 1] + L[Y.oZB + ZS * k + 2] * L[Y.oDZV + ZS * k + 2]);
         v += -2.0 * P.w_s * (X.R.s_total - L[Y.oZB + ZS * k]) / (X.den * X.den) * L[Y.oDZV + ZS * k];
         v += 2.0 * P.w_u * (L[Y.oZB + ZS * k + 5] * L[Y.oDZV + ZS * k + 5] + L[Y.oZB + ZS * k + 6] * L[Y.oDZV + ZS * k + 6]);
@@ -1899,6 +1916,7 @@ __device__ inline ldsd* lds_p(const Ctx& X) { return X.L; }
 // one chunk NLP (trajectory_planning.py:351-390) at X.x0, X.st, X.fin, X.N, set by the caller: the plan is
 // left in the LDS block (ZB); returns the status, the interior-point iterations and QPs in *total_out, *nq_out
 __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) {
+    const int ln = X.ln;            // the lane, once (the context lives in private memory)
     const int N = UNI(X.N);
     X.den = fmax(1.0, X.R.s_total - X.x0[0]);
     X.nu[0] = X.nu[1] = 0.0;
@@ -1907,7 +1925,7 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
     const Layout& Y = X.Y;
     // initial guess (:357-376)
     const double dss = (X.st - X.x0[0]) / N;
-    for (int k = X.ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += WAVE) {
 #pragma unroll
         for (int i = 0; i < NZ; ++i) L[Y.oZB + ZS * k + i] = 0.0;
         L[Y.oZB + ZS * k + 0] = k == N ? X.st : X.x0[0] + k * dss;
@@ -1939,7 +1957,7 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
         if (X.dbg & 32) multipliers(X);
         multipliers(X);
         double full = 0.0, mu_l = 0.0;
-        for (int k = X.ln; k <= N; k += WAVE) {
+        for (int k = ln; k <= N; k += WAVE) {
 #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 const double d = (k < N || i < 5) ? L[Y.oZ + ZS * k + i] : 0.0;
@@ -1959,7 +1977,7 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
         sync();
         double alpha = 1.0;
         if (full > LS_FULL) {
-            for (int k = X.ln; k <= N; k += WAVE) L[Y.oVL + k] = frozen ? L[Y.oVLIM + k] : route_vmax(X.R, L[Y.oZB + ZS * k]);
+            for (int k = ln; k <= N; k += WAVE) L[Y.oVL + k] = frozen ? L[Y.oVLIM + k] : route_vmax(X.R, L[Y.oZB + ZS * k]);
             sync();
             double f0, v0;
             cost_viol(X, 0.0, &f0, &v0);
@@ -1978,7 +1996,7 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
             }
         }
         double step = 0.0, back2 = 0.0, fin = 1.0;
-        for (int k = X.ln; k <= N; k += WAVE)
+        for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 if (k == N && i >= 5) continue;
@@ -1992,7 +2010,7 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
         back2 = wmax(back2);
         fin = wmin(fin);
         if (fin == 0.0) { status = PLAN_NUMERICAL; break; }
-        for (int k = X.ln; k <= N; k += WAVE)
+        for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
             for (int i = 0; i < NZ; ++i) {
                 if (k == N && i >= 5) continue;
@@ -2005,11 +2023,11 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
         if (step <= X.P.sqp_tol) { status = frozen ? PLAN_FROZEN_LIMITS : PLAN_OK; break; }
         if (since >= 2 && back2 <= CYCLE_REL * step) {
             if (frozen) break;
-            for (int k = X.ln; k <= N; k += WAVE)
+            for (int k = ln; k <= N; k += WAVE)
                 L[Y.oVLIM + k] = fmin(route_vmax(X.R, L[Y.oZB + ZS * k]), route_vmax(X.R, L[Y.oZ2 + ZS * k]));
             frozen = true;
             since = -1;
-            for (int k = X.ln; k <= N; k += WAVE)
+            for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
                 for (int i = 0; i < NZ; ++i) L[Y.oZ2 + ZS * k + i] = L[Y.oZB + ZS * k + i];
             sync();
@@ -2017,7 +2035,7 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
     }
     if (status == PLAN_FROZEN_LIMITS) {
         double bad = 0.0;
-        for (int k = X.ln; k <= N; k += WAVE)
+        for (int k = ln; k <= N; k += WAVE)
             if (L[Y.oZB + ZS * k + 4] + (k < N ? L[Y.oZB + ZS * k + 7] : 0.0) > route_vmax(X.R, L[Y.oZB + ZS * k]) + 1e-9)
                 bad = 1.0;
         if (wmax(bad) > 0.0) status = PLAN_NOT_CONVERGED;
