@@ -1103,8 +1103,7 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
         auto step = [&](const SolBk& c, int k) {
             double h = c.h;                       // h_rh = gw_rh + sum_l B(l, rh) p_l
             dot5_lanes(h, p, c.Br);
-            if (ln < 2) L[odz + ZS * k + 5 + ln] = h;
-            if (ln == 2) L[odz + ZS * k + 7] = c.h2;
+            if (ln < 3) L[odz + ZS * k + 5 + ln] = ln < 2 ? h : c.h2;    // the w slots: h_0, h_1, h2 (one store)
             double v = c.gx;
             dot5_lanes(v, p, c.Ac);
             dot2_lanes(v, h, c.Kc[0], c.Kc[1]);   // + K(0, me) h_0 + K(1, me) h_1
@@ -1147,8 +1146,8 @@ __device__ void solve_core(const Ctx& X, int ogl, int odz) {
             dot2_lanes(xn, w, c.b0, c.b1);        // + B(me, 0) w_0 + B(me, 1) w_1
             // stage k overwritten after every lane has read its feed-forward term (program order within the
             // wave; the emulation's broadcasts above are barriers)
-            if (ln < 5) L[odz + ZS * k + ln] = x;
-            if (ln < 3) L[odz + ZS * k + 5 + ln] = w;
+            // x_0..4 from lanes 0..4, w_0..2 from lanes 16..18 (row 1's copies of lanes 0..2): one store
+            if (ln < 5 || (ln >= 16 && ln < 19)) L[odz + ZS * k + (ln < 16 ? ln : ln - 11)] = ln < 16 ? x : w;
             x = xn;
         };
         // two stages per trip, alternating buffers; a stage's feed-forward slots are read before the stage
@@ -1846,8 +1845,11 @@ __device__ void multipliers(Ctx& X) {
 }
 
 // the NLP's cost (:128-170) and L1 violation at ZB + alpha * DZV (stage-parallel, reduced)
-__device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
-    const int ln = X.ln;            // the lane, once (the context lives in private memory)
+// cost and violation at ZB + alpha DZV.  GS < WAVE: each group of GS lanes (GS >= N + 1) evaluates its own
+// alpha, the sums reduced within the group -- the same butterfly as wsum's last log2(GS) levels, whose first
+// levels only add the idle lanes' exact zeros, so every group's sums are wsum's for its alpha bit for bit
+__device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol, int GS = WAVE) {
+    const int ln = X.ln & (GS - 1);      // the lane within its group
     PHASE(PH_LSEARCH);
     const int N = UNI(X.N);
     ldsd* L = X.L;
@@ -1857,7 +1859,7 @@ __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
     double c = 0.0, v = 0.0;
     if (ln == 0)
         for (int i = 0; i < 5; ++i) v += fabs(zv(0, i) - X.x0[i]);
-    for (int k = ln; k <= N; k += WAVE) {
+    for (int k = ln; k <= N; k += GS) {
         double x[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) x[i] = zv(k, i);
@@ -1890,8 +1892,12 @@ __device__ void cost_viol(const Ctx& X, double alpha, double* f, double* viol) {
         add(k == N && !X.fin, x[0] - X.st / 2.0);
         if (k == N && X.fin) v += fabs(x[0] - X.st) + fabs(x[4]);
     }
-    *f = wsum(c);
-    *viol = wsum(v);
+    for (int o = GS >> 1; o > 0; o >>= 1) {
+        c += __shfl_xor(c, o, WAVE);
+        v += __shfl_xor(v, o, WAVE);
+    }
+    *f = c;
+    *viol = v;
 }
 
 __device__ double cost_dir(const Ctx& X) {
@@ -1987,12 +1993,23 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
             ++nh;
             double m0 = -INFINITY;
             for (int i = 0; i < (nh < LS_MEMORY ? nh : LS_MEMORY); ++i) m0 = fmax(m0, hf[i] + mu_m * hv[i]);
-            for (int ls = 0; ls < LS_STEPS; ++ls) {
+            // backtracking alpha = 1, 1/2, ...: G = WAVE / GS trials at once, trial ls + g on lane group g (the
+            // halvings are exact, so group g's alpha * 2^-g is the serial loop's alpha); the first accepted trial
+            // in order wins, the last one (LS_STEPS - 1) unconditionally, as in the serial loop
+            const int GS = N + 1 <= 16 ? 16 : (N + 1 <= 32 ? 32 : WAVE), G = WAVE / GS, g = ln / GS;
+            const double gsc = g == 0 ? 1.0 : (g == 1 ? 0.5 : (g == 2 ? 0.25 : 0.125)), gstep = G == 4 ? 0.0625 : (G == 2 ? 0.25 : 0.5);
+            for (int ls = 0;; ls += G) {
+                const double ag = alpha * gsc;
                 double f1, v1;
-                if (X.dbg & 64) cost_viol(X, alpha, &f1, &v1);
-                cost_viol(X, alpha, &f1, &v1);
-                if (f1 + mu_m * v1 <= m0 + LS_ARMIJO * alpha * dd || ls == LS_STEPS - 1) break;
-                alpha *= 0.5;
+                if (X.dbg & 64) cost_viol(X, ag, &f1, &v1, GS);
+                cost_viol(X, ag, &f1, &v1, GS);
+                const bool acc = ls + g < LS_STEPS && (f1 + mu_m * v1 <= m0 + LS_ARMIJO * ag * dd || ls + g == LS_STEPS - 1);
+                const double first = wmin(acc ? (double)g : (double)G);
+                if (first < (double)G) {
+                    alpha *= first == 0.0 ? 1.0 : (first == 1.0 ? 0.5 : (first == 2.0 ? 0.25 : 0.125));
+                    break;
+                }
+                alpha *= gstep;
             }
         }
         double step = 0.0, back2 = 0.0, fin = 1.0;
