@@ -470,28 +470,54 @@ __device__ inline RowAt row_at(const ldsd* L, int oZB, int q, int N, int fin) {
     return r;
 }
 
-// Gaussian elimination with partial pivoting on a 5x5 system with NC right-hand sides (registers)
+// Gaussian elimination with partial pivoting on a 5x5 system with NC right-hand sides, in registers: the pivot
+// row is found and swapped by selects (every candidate row compared, the one chosen exchanged), so no array is
+// indexed at run time (a run-time row index would put M and R in scratch memory); columns left of the pivot
+// column are never read again and are not exchanged.  The first largest |M(i, c)| wins, as in the oracle.
 template <int NC>
 __device__ bool solve5(double M[25], double R[5 * NC]) {
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
         int pr = c;
-        for (int i = c + 1; i < 5; ++i)
-            if (fabs(M[5 * i + c]) > fabs(M[5 * pr + c])) pr = i;
-        if (M[5 * pr + c] == 0.0) return false;
-        if (pr != c) {
-            for (int j = 0; j < 5; ++j) { const double t = M[5 * c + j]; M[5 * c + j] = M[5 * pr + j]; M[5 * pr + j] = t; }
-            for (int j = 0; j < NC; ++j) { const double t = R[NC * c + j]; R[NC * c + j] = R[NC * pr + j]; R[NC * pr + j] = t; }
+        double best = fabs(M[5 * c + c]);
+#pragma unroll
+        for (int i = c + 1; i < 5; ++i) {
+            const double a = fabs(M[5 * i + c]);
+            pr = a > best ? i : pr;
+            best = a > best ? a : best;
         }
+#pragma unroll
+        for (int i = c + 1; i < 5; ++i) {
+            const bool sw = pr == i;
+#pragma unroll
+            for (int j = c; j < 5; ++j) {
+                const double t = M[5 * c + j];
+                M[5 * c + j] = sw ? M[5 * i + j] : t;
+                M[5 * i + j] = sw ? t : M[5 * i + j];
+            }
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                const double t = R[NC * c + j];
+                R[NC * c + j] = sw ? R[NC * i + j] : t;
+                R[NC * i + j] = sw ? t : R[NC * i + j];
+            }
+        }
+        if (M[5 * c + c] == 0.0) return false;
+#pragma unroll
         for (int i = c + 1; i < 5; ++i) {
             const double f = M[5 * i + c] / M[5 * c + c];
+#pragma unroll
             for (int j = c; j < 5; ++j) M[5 * i + j] -= f * M[5 * c + j];
+#pragma unroll
             for (int j = 0; j < NC; ++j) R[NC * i + j] -= f * R[NC * c + j];
         }
     }
+#pragma unroll
     for (int c = 4; c >= 0; --c)
+#pragma unroll
         for (int j = 0; j < NC; ++j) {
             double v = R[NC * c + j];
+#pragma unroll
             for (int k = c + 1; k < 5; ++k) v -= M[5 * c + k] * R[NC * k + j];
             R[NC * c + j] = v / M[5 * c + c];
         }
