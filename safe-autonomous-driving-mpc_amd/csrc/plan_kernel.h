@@ -22,6 +22,8 @@ namespace {
 constexpr int WAVE = 64;
 constexpr int NZ = 8;             // stage variables: x (s, d, o, k, v), w (u1, u2, S)
 constexpr int NR = 11;            // rows per stage at most
+constexpr int RS = 11;            // row slots per stage in LDS: one per row kind (kind_slot), so every row visit
+                                  // has a compile-time slot; a stage's missing kinds leave their slots unused
 constexpr int NH = 36;            // packed symmetric 8x8
 // LDS strides of the per-stage 8-vectors and stage Hessians: one double of padding each, so the lanes of a
 // stage-parallel loop (lane k on stage k) spread over the LDS banks (a stride of 8 doubles = 16 dwords put
@@ -80,7 +82,7 @@ inline void route_grid(const double* s, int M, int T, int* grid, double* ginv) {
 struct Layout {
     int NP;
     int oAB, oH, oGQ, oG, oK, oL, oEZ, oZ, oS, oLAM, oGL, oDZ, oDSA, oDLA, oDS, oDL, oMY, oMLAT, oZB,
-        oZ2, oDZV, oPI, oVLIM, oVL, oACT, oTACT, oSC, oWK;
+        oZ2, oDZV, oPI, oVLIM, oVL, oACT, oTACT, oSC;
     int oY, oTLAM, oTZ;
     int total;
 };
@@ -96,19 +98,19 @@ __host__ __device__ Layout make_layout(int Nmax) {
                                      // row weights at the 8 entries rows touch (hs_slot; elsewhere it is H + delta I), then
                                      // 1 / HT(7, 7)
     y.oGQ = o; o += ZS * np;
-    y.oG = o; o += NR * np;
+    y.oG = o; o += RS * np;
     y.oK = o; o += 15 * np;
     y.oL = o; o += 6 * np;
     y.oEZ = o; o += 2 * ZS * np;
     y.oZ = o; o += ZS * np;
-    y.oS = o; o += NR * np;
-    y.oLAM = o; o += NR * np;
+    y.oS = o; o += RS * np;
+    y.oLAM = o; o += RS * np;
     y.oGL = o; o += ZS * np;
     y.oDZ = o; o += ZS * np;
-    y.oDSA = o; o += NR * np;
-    y.oDLA = o; o += NR * np;
-    y.oDS = o; o += NR * np;
-    y.oDL = o; o += NR * np;
+    y.oDSA = o; o += RS * np;
+    y.oDLA = o; o += RS * np;
+    y.oDS = o; o += RS * np;
+    y.oDL = o; o += RS * np;
     y.oMY = o; o += 5 * np;
     y.oMLAT = o; o += 2 * np;
     y.oZB = o; o += ZS * np;
@@ -116,13 +118,12 @@ __host__ __device__ Layout make_layout(int Nmax) {
     y.oDZV = o; o += ZS * np;
     y.oVLIM = o; o += np;
     y.oVL = o; o += np;
-    y.oACT = o; o += np;             // active-row bit masks (11 bits), stored as doubles
+    y.oACT = o; o += np;             // active-row bit masks (bit = slot, kind_slot), stored as doubles
     y.oTACT = o; o += np;
     y.oSC = o; o += 16;              // scalars shared by the wave
 #ifdef PLAN_PROF
     o += 16;                         // phase counters of the diagnostic build
 #endif
-    y.oWK = o; o += 96;              // factorisation work area: P (25), M (64)
     y.oY = y.oDSA;
     y.oTLAM = y.oDLA;
     y.oTZ = y.oDS;
@@ -370,7 +371,10 @@ __host__ __device__ constexpr int row_kind(int k, int N, int fin, int j) {
 // (for_rows), where each kind, and with it the indices of its nonzero coefficients, is a compile-time
 // constant.  Adding only the nonzero terms, in the same order, gives the dense loops' values (a skipped
 // term is an exact zero).
-__device__ __forceinline__ bool row_on(int kind, int k, int N, int fin) {
+// the LDS slot of a row kind: its own, except the intermediate chunk's terminal row (k = N only), which takes
+// the u1-min slot (no stage has both), so a stage's rows fit in NR slots in row order
+__host__ __device__ constexpr int kind_slot(int kind) { return kind == ROW_STERM ? ROW_U1MIN : kind; }
+__host__ __device__ constexpr bool row_on(int kind, int k, int N, int fin) {
     switch (kind) {
         case ROW_VMIN: case ROW_VMAX: return !(fin && k == N);
         case ROW_LATP: case ROW_LATM: return !(fin && k == N) && k > 0;
@@ -400,8 +404,8 @@ __device__ __forceinline__ RowSp row_sp(int kind, bool has_w, double kb, double 
         default: return {0, 0, 1.0, 0.0, false};        // ROW_STERM
     }
 }
-// f(kind, j, on) for every row kind of stage k, in storage order: j = the row's slot when on (the stage has
-// the row), else a valid slot of the stage (clamped) whose values the body must not use.  The body runs
+// f(kind, j, on) for every row kind of stage k, in storage order: j = the row's slot (kind_slot, a compile-time
+// constant), on = the stage has the row (else the slot's values are not the body's to use).  The body runs
 // unconditionally -- loads, divisions and all -- and applies its results under `on` (selects, masked stores):
 // no branch per kind, so the scheduler overlaps the rows' independent chains (one lane serves a stage, so
 // the rows are its serial work); every on-row value is computed by the same operations as before.
@@ -410,9 +414,8 @@ __device__ __forceinline__ RowSp row_sp(int kind, bool has_w, double kb, double 
 template <int KIND, class F>
 __device__ __forceinline__ void for_rows_from(int k, int N, int fin, int j, F& f) {
     if constexpr (KIND <= ROW_STERM) {
-        const bool on = row_on(KIND, k, N, fin);
-        f(KIND, j < NR ? j : NR - 1, on);
-        for_rows_from<KIND + 1>(k, N, fin, j + (on ? 1 : 0), f);
+        f(KIND, kind_slot(KIND), row_on(KIND, k, N, fin));
+        for_rows_from<KIND + 1>(k, N, fin, j, f);
     }
 }
 template <class F>
@@ -426,9 +429,9 @@ __device__ __forceinline__ double sp_dot(const RowSp& r, double g, const double 
     return v;
 }
 
-// Row-parallel visits: slot q = NR k + j of the row arrays (S, LAM, G, DS, ...), lane q, q + 64, ...: the
-// interior point's per-row divisions and ratio tests run on (N + 1) NR / 64 slots per lane instead of a
-// stage's NR rows on each of N + 1 lanes.  The row's stage, kind and coefficients come arithmetically from
+// Row-parallel visits: slot q = RS k + j of the row arrays (S, LAM, G, DS, ...), lane q, q + 64, ...: the
+// interior point's per-row divisions and ratio tests run on (N + 1) RS / 64 slots per lane instead of a
+// stage's rows on each of N + 1 lanes.  The row's stage, kind and coefficients come arithmetically from
 // q (no branch per kind): the same values row_sp gives (c0 = -vb vb for ROW_LATP is (-vb) vb exactly,
 // c1 = (-2 kb) vb likewise), so every row value is formed by the same operations as in for_rows.
 struct RowAt {
@@ -436,24 +439,24 @@ struct RowAt {
     bool on, two;
     double c0, c1;
 };
-// the kinds of a stage's slots 0..10, 4 bits per slot (slots past the stage's rows: ROW_STERM), for the four
-// stage shapes: first stage (k = 0 < N), interior, last stage of the final chunk, last stage of an intermediate
-// chunk -- row_kind tabulated, so a slot's kind is a shift of a selected constant instead of a select chain
-__host__ __device__ constexpr unsigned long long kind_tab(int k, int N, int fin) {
-    unsigned long long t = 0;
-    for (int j = 0; j < NR; ++j)
-        t |= (unsigned long long)(j < stage_nrows(k, N, fin) ? row_kind(k, N, fin, j) : ROW_STERM) << (4 * j);
-    return t;
+// the slots a stage's rows occupy, one bit per slot, for the four stage shapes: first stage (k = 0 < N),
+// interior, last stage of the final chunk, last stage of an intermediate chunk (row_on tabulated)
+__host__ __device__ constexpr unsigned on_tab(int k, int N, int fin) {
+    unsigned m = 0;
+    for (int kind = 0; kind <= ROW_STERM; ++kind) m |= row_on(kind, k, N, fin) ? 1u << kind_slot(kind) : 0u;
+    return m;
 }
-constexpr unsigned long long KIND_FIRST = kind_tab(0, 2, 0), KIND_MID = kind_tab(1, 2, 0), KIND_LASTF = kind_tab(2, 2, 1),
-                             KIND_LASTI = kind_tab(2, 2, 0);
+// the kind in slot j of stage k (the slot it shares decides: the terminal row at k = N)
+__host__ __device__ constexpr int slot_kind(int j, int k, int N) { return (k == N && j == ROW_U1MIN) ? ROW_STERM : j; }
+constexpr unsigned ON_FIRST = on_tab(0, 2, 0), ON_MID = on_tab(1, 2, 0), ON_LASTF = on_tab(2, 2, 1), ON_LASTI = on_tab(2, 2, 0);
+__device__ inline unsigned stage_on(int k, int N, int fin) {
+    return k == N ? (fin ? ON_LASTF : ON_LASTI) : (k == 0 ? ON_FIRST : ON_MID);
+}
 __device__ inline RowAt row_at(const ldsd* L, int oZB, int q, int N, int fin) {
     RowAt r;
-    const int k = q / NR, j = q - NR * k;
+    const int k = q / RS, j = q - RS * k, kind = slot_kind(j, k, N);
     r.k = k;
-    r.on = j < stage_nrows(k, N, fin);
-    const unsigned long long tab = k == N ? (fin ? KIND_LASTF : KIND_LASTI) : (k == 0 ? KIND_FIRST : KIND_MID);
-    const int kind = (int)((tab >> (4 * j)) & 15ull);
+    r.on = (stage_on(k, N, fin) >> j) & 1u;
     // nibble tables over the kinds (ROW_VMIN .. ROW_STERM): first and second coefficient's variable
     constexpr unsigned long long I0TAB = 0x076655333344ull;   // kind 0..11: 4 4 3 3 3 3 5 5 6 6 7 0
     constexpr unsigned long long I1TAB = 0x076655334477ull;   // kind 0..11: 7 7 4 4 3 3 5 5 6 6 7 0
@@ -856,11 +859,11 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
                 }
             }
         }
-        const int nr = stage_nrows(k, N, fin_u);
         const double kk = x[3], v = x[4];
-        for (int j = 0; j < nr; ++j) {
+        const unsigned son = stage_on(k, N, fin_u);
+        for (int j = 0; j < RS; ++j) {             // slot j (kind_slot); a slot without a row gets 0
             double gv = 0.0;
-            switch (row_kind(k, N, fin_u, j)) {
+            switch ((son >> j) & 1u ? slot_kind(j, k, N) : -1) {
                 case ROW_VMIN: gv = v + sl - P.v_min; break;
                 case ROW_VMAX: gv = (frozen ? L[Y.oVLIM + k] : route_vmax(X.R, x[0])) - (v + sl); break;
                 case ROW_LATP: gv = P.a_max - kk * v * v; break;
@@ -872,9 +875,10 @@ __device__ bool build_qp(Ctx& X, bool frozen, bool exact) {
                 case ROW_U2MIN: gv = u2 - P.u_min[1]; break;
                 case ROW_U2MAX: gv = P.u_max[1] - u2; break;
                 case ROW_S: gv = sl; break;
-                default: gv = x[0] - X.st / 2.0; break;
+                case ROW_STERM: gv = x[0] - X.st / 2.0; break;
+                default: gv = 0.0; break;
             }
-            L[Y.oG + NR * k + j] = gv;
+            L[Y.oG + RS * k + j] = gv;
         }
         if (exact && k > 0 && !(fin_u && k == N)) {
             const double lp = L[Y.oMLAT + 2 * k], lm = L[Y.oMLAT + 2 * k + 1];
@@ -904,7 +908,7 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
     if (mode == 0) {
         // the barrier weights w = lam / s, row-parallel, into DS (free at the top of an interior-point
         // iteration: the previous step has been taken)
-        for (int q = ln; q < (N + 1) * NR; q += WAVE) {
+        for (int q = ln; q < (N + 1) * RS; q += WAVE) {
             const RowAt r = row_at(L, Y.oZB, q, N, fin_u);
             const double w = L[Y.oLAM + q] / L[Y.oS + q];
             if (r.on) L[Y.oDS + q] = w;
@@ -932,7 +936,7 @@ __device__ void stage_hess_par(Ctx& X, int mode) {
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         const unsigned act = mode == 0 ? 0u : (unsigned)L[Y.oTACT + k];
         for_rows(k, N, fin_u, [&](int kind, int j, bool on) {
-            const double w = mode == 0 ? L[Y.oDS + NR * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
+            const double w = mode == 0 ? L[Y.oDS + RS * k + j] : (((act >> j) & 1u) ? RHO : 0.0);
             const bool use = on && w != 0.0;
             const RowSp r = row_sp(kind, k < N, kb, vb);
             const int a = hx(r.i0, r.i0), b = hx(r.i0, r.i1), c = hx(r.i1, r.i1);
@@ -1427,7 +1431,7 @@ __device__ int eqp(Ctx& X, double scale) {
     const double e0 = X.e[0], e1 = X.e[1];
     for (int k = ln; k <= N; k += WAVE)
 #pragma unroll
-        for (int j = 0; j < NR; ++j) L[Y.oY + NR * k + j] = act_bit(X, Y.oTACT, k, j) ? L[Y.oTLAM + NR * k + j] : 0.0;
+        for (int j = 0; j < RS; ++j) L[Y.oY + RS * k + j] = act_bit(X, Y.oTACT, k, j) ? L[Y.oTLAM + RS * k + j] : 0.0;
     sync();
     if (!factor_reg(X, 1)) return -1;
     const double delta = X.delta;
@@ -1443,7 +1447,7 @@ __device__ int eqp(Ctx& X, double scale) {
             for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
                 const bool use = on && ((act >> j) & 1u);
                 const RowSp r = row_sp(kind, k < N, kb, vb);
-                const double f = RHO * sp_dot(r, L[Y.oG + NR * k + j], z) - L[Y.oY + NR * k + j];
+                const double f = RHO * sp_dot(r, L[Y.oG + RS * k + j], z) - L[Y.oY + RS * k + j];
                 const double g0 = g[r.i0] + f * r.c0;
                 g[r.i0] = use ? g0 : g[r.i0];
                 if (r.two) {
@@ -1468,9 +1472,9 @@ __device__ int eqp(Ctx& X, double scale) {
             const unsigned act = (unsigned)L[Y.oTACT + k];
             for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
                 const bool use = on && ((act >> j) & 1u);
-                const double d = RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
-                const double y = L[Y.oY + NR * k + j] - d;
-                if (use) L[Y.oY + NR * k + j] = y;
+                const double d = RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + RS * k + j], z);
+                const double y = L[Y.oY + RS * k + j] - d;
+                if (use) L[Y.oY + RS * k + j] = y;
                 upd = use ? fmax(upd, fabs(d)) : upd;
                 ym = use ? fmax(ym, fabs(y)) : ym;
             });
@@ -1493,10 +1497,10 @@ __device__ int eqp(Ctx& X, double scale) {
         for (int u = 0; u < NZ; ++u) z[u] = L[Y.oTZ + ZS * k + u];
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
-            const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
-            const double y = L[Y.oY + NR * k + j];
+            const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + RS * k + j], z);
+            const double y = L[Y.oY + RS * k + j];
             const bool in = (mask >> j) & 1u;
-            if (on) L[Y.oTLAM + NR * k + j] = in ? y : 0.0;
+            if (on) L[Y.oTLAM + RS * k + j] = in ? y : 0.0;
             const bool flip = on && (in ? (y < -tl || fabs(rv) > tr) : rv < -tr);
             mask = flip ? (mask ^ (1u << j)) : mask;
             bad += flip ? 1 : 0;
@@ -1519,7 +1523,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
     const int N = UNI(X.N);
     ldsd* L = X.L;
     const Layout Y = uni_layout(X.Y);
-    const int nq = (N + 1) * NR, nzq = (N + 1) * ZS;      // row slots, stage-variable slots
+    const int nq = (N + 1) * RS, nzq = (N + 1) * ZS;      // row slots, stage-variable slots
     // the context's scalars the iterations read, taken once (the context lives in private memory)
     const int dbg = UNI(X.dbg), fin_c = UNI(X.fin), max_iter = UNI(X.P.max_iter);
     const double tol = X.P.tol, e0 = X.e[0], e1 = X.e[1];
@@ -1532,10 +1536,10 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
             if (!resume) {
-                const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + NR * k + j], z);
+                const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + RS * k + j], z);
                 if (on) {
-                    L[Y.oS + NR * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
-                    L[Y.oLAM + NR * k + j] = 1.0;
+                    L[Y.oS + RS * k + j] = (rv > 0.0 ? rv : 0.0) + SHIFT0;
+                    L[Y.oLAM + RS * k + j] = 1.0;
                 }
             }
             m += on ? 1 : 0;
@@ -1549,11 +1553,11 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
         double mu = 0.0;
         PhOpen(ph_red, X, PH_IRED);
         for (int k = ln; k <= N; k += WAVE) {
-            const int nr = stage_nrows(k, N, fin_c);
+            const unsigned son = stage_on(k, N, fin_c);
 #pragma unroll
-            for (int j = 0; j < NR; ++j) {      // every slot, the stage's rows applied (see for_rows)
-                const double t = mu + L[Y.oS + NR * k + j] * L[Y.oLAM + NR * k + j];
-                mu = j < nr ? t : mu;
+            for (int j = 0; j < RS; ++j) {      // every slot, the stage's rows applied (see for_rows)
+                const double t = mu + L[Y.oS + RS * k + j] * L[Y.oLAM + RS * k + j];
+                mu = (son >> j) & 1u ? t : mu;
             }
         }
         mu = wsum(mu) / m;
@@ -1588,12 +1592,12 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                 am = wmin(am);
                 double mua = 0.0;
                 for (int k = ln; k <= N; k += WAVE) {
-                    const int nr = stage_nrows(k, N, fin_c);
+                    const unsigned son = stage_on(k, N, fin_c);
 #pragma unroll
-                    for (int j = 0; j < NR; ++j) {
-                        const double t = mua + (L[Y.oS + NR * k + j] + am * L[Y.oDSA + NR * k + j]) *
-                                                   (L[Y.oLAM + NR * k + j] + am * L[Y.oDLA + NR * k + j]);
-                        mua = j < nr ? t : mua;
+                    for (int j = 0; j < RS; ++j) {
+                        const double t = mua + (L[Y.oS + RS * k + j] + am * L[Y.oDSA + RS * k + j]) *
+                                                   (L[Y.oLAM + RS * k + j] + am * L[Y.oDLA + RS * k + j]);
+                        mua = (son >> j) & 1u ? t : mua;
                     }
                 }
                 mua = wsum(mua) / m;
@@ -1624,7 +1628,7 @@ __device__ int ipm(Ctx& X, int* iters, bool resume, double* phi_io) {
                     const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
                     for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
                         const RowSp r = row_sp(kind, k < N, kb, vb);
-                        const double f = L[Y.oDS + NR * k + j];
+                        const double f = L[Y.oDS + RS * k + j];
                         const double g0 = g[r.i0] - f * r.c0;
                         g[r.i0] = on ? g0 : g[r.i0];
                         if (r.two) {
@@ -1710,7 +1714,7 @@ __device__ void accept_polish(const Ctx& X, bool with_act) {
 #pragma unroll
         for (int u = 0; u < NZ; ++u) L[Y.oZ + ZS * k + u] = L[Y.oTZ + ZS * k + u];
 #pragma unroll
-        for (int j = 0; j < NR; ++j) L[Y.oLAM + NR * k + j] = L[Y.oTLAM + NR * k + j];
+        for (int j = 0; j < RS; ++j) L[Y.oLAM + RS * k + j] = L[Y.oTLAM + RS * k + j];
         if (with_act) L[Y.oACT + k] = L[Y.oTACT + k];
     }
     sync();
@@ -1718,11 +1722,11 @@ __device__ void accept_polish(const Ctx& X, bool with_act) {
 
 // interior-point classification (s < lam) of stage k as a bit mask
 __device__ double ipm_mask(const Ctx& X, int k) {
-    const int nr = stage_nrows(k, X.N, X.fin);
+    const unsigned son = stage_on(k, X.N, X.fin);
     unsigned m = 0;
 #pragma unroll
-    for (int j = 0; j < NR; ++j)
-        if (j < nr && X.L[X.Y.oS + NR * k + j] < X.L[X.Y.oLAM + NR * k + j]) m |= 1u << j;
+    for (int j = 0; j < RS; ++j)
+        if (((son >> j) & 1u) && X.L[X.Y.oS + RS * k + j] < X.L[X.Y.oLAM + RS * k + j]) m |= 1u << j;
     return (double)m;
 }
 
@@ -1735,9 +1739,9 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
     const Layout& Y = X.Y;
     double scale = 1.0;
     for (int k = ln; k <= N; k += WAVE) {
-        const int nr = stage_nrows(k, N, fin_u);
+        const unsigned son = stage_on(k, N, fin_u);
 #pragma unroll
-        for (int j = 0; j < NR; ++j) scale = j < nr ? fmax(scale, fabs(L[Y.oG + NR * k + j])) : scale;
+        for (int j = 0; j < RS; ++j) scale = (son >> j) & 1u ? fmax(scale, fabs(L[Y.oG + RS * k + j])) : scale;
     }
     scale = wmax(scale);
     *iters = 0;
@@ -1745,7 +1749,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
         for (int k = ln; k <= N; k += WAVE) {
             L[Y.oTACT + k] = L[Y.oACT + k];
 #pragma unroll
-            for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
+            for (int j = 0; j < RS; ++j) L[Y.oTLAM + RS * k + j] = L[Y.oLAM + RS * k + j];
         }
         sync();
         for (int round = 0; round < WARM_ROUNDS; ++round) {
@@ -1765,7 +1769,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
         for (int k = ln; k <= N; k += WAVE) {
             L[Y.oTACT + k] = ipm_mask(X, k);
 #pragma unroll
-            for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
+            for (int j = 0; j < RS; ++j) L[Y.oTLAM + RS * k + j] = L[Y.oLAM + RS * k + j];
         }
         sync();
         for (int round = 0; round < CHECK_ROUNDS; ++round) {
@@ -1783,7 +1787,7 @@ __device__ int qp_solve(Ctx& X, bool have_cls, int* iters) {
     for (int k = ln; k <= N; k += WAVE) {
         L[Y.oTACT + k] = ipm_mask(X, k);
 #pragma unroll
-        for (int j = 0; j < NR; ++j) L[Y.oTLAM + NR * k + j] = L[Y.oLAM + NR * k + j];
+        for (int j = 0; j < RS; ++j) L[Y.oTLAM + RS * k + j] = L[Y.oLAM + RS * k + j];
     }
     sync();
     for (int round = 0; round < POLISH_ROUNDS; ++round) {
@@ -1817,7 +1821,7 @@ __device__ void multipliers(Ctx& X) {
         const double kb = L[Y.oZB + ZS * k + 3], vb = L[Y.oZB + ZS * k + 4];
         for_rows(k, N, fin_u, [&](int kind, int j, bool on) {
             const RowSp r = row_sp(kind, k < N, kb, vb);
-            const double l = L[Y.oLAM + NR * k + j];
+            const double l = L[Y.oLAM + RS * k + j];
             const double g0 = g[r.i0] - l * r.c0;
             g[r.i0] = on ? g0 : g[r.i0];
             if (r.two) {
@@ -1999,9 +2003,9 @@ __device__ __forceinline__ int solve_chunk(Ctx& X, int* total_out, int* nq_out) 
             if (k < N)
 #pragma unroll
                 for (int i = 0; i < 5; ++i) mu_l = fmax(mu_l, 2.0 * fabs(L[Y.oMY + 5 * k + i]));
-            const int nr = stage_nrows(k, N, X.fin);
+            const unsigned son = stage_on(k, N, X.fin);
 #pragma unroll
-            for (int j = 0; j < NR; ++j) mu_l = j < nr ? fmax(mu_l, 2.0 * fabs(L[Y.oLAM + NR * k + j])) : mu_l;
+            for (int j = 0; j < RS; ++j) mu_l = (son >> j) & 1u ? fmax(mu_l, 2.0 * fabs(L[Y.oLAM + RS * k + j])) : mu_l;
         }
         full = wmax(full);
         mu_m = fmax(mu_m, wmax(mu_l));

@@ -109,13 +109,13 @@ static int rows_selftest() {
                 L[ZS * k + 4] = 1.3 + 0.71 * k;                  // vb
             }
             for (int k = 0; k <= N; ++k) {
-                bool seen[NR] = {false};
+                bool seen[RS] = {false};
                 const double kb = L[ZS * k + 3], vb = L[ZS * k + 4];
                 for_rows(k, N, fin, [&](int kind, int j, bool on) {
                     if (!on) return;
                     seen[j] = true;
                     const RowSp r = row_sp(kind, k < N, kb, vb);
-                    const RowAt a = row_at(L.data(), 0, NR * k + j, N, fin);
+                    const RowAt a = row_at(L.data(), 0, RS * k + j, N, fin);
                     ++checked;
                     const bool ok = a.k == k && a.on && a.i0 == r.i0 && a.two == r.two &&
                                     std::memcmp(&a.c0, &r.c0, 8) == 0 && (!r.two || (a.i1 == r.i1 && std::memcmp(&a.c1, &r.c1, 8) == 0));
@@ -123,8 +123,8 @@ static int rows_selftest() {
                         fprintf(stderr, "N=%d fin=%d k=%d j=%d kind=%d: row_at k %d i0 %d i1 %d two %d c0 %g c1 %g vs i0 %d i1 %d two %d c0 %g c1 %g\n",
                                 N, fin, k, j, kind, a.k, a.i0, a.i1, a.two, a.c0, a.c1, r.i0, r.i1, r.two, r.c0, r.c1);
                 });
-                for (int j = 0; j < NR; ++j)
-                    if (!seen[j] && row_at(L.data(), 0, NR * k + j, N, fin).on && bad++ < 10)
+                for (int j = 0; j < RS; ++j)
+                    if (!seen[j] && row_at(L.data(), 0, RS * k + j, N, fin).on && bad++ < 10)
                         fprintf(stderr, "N=%d fin=%d k=%d j=%d: row_at says on, for_rows has no row there\n", N, fin, k, j);
             }
         }
