@@ -1473,8 +1473,8 @@ __device__ int eqp(Ctx& X, double scale) {
             for_rows(k, N, fin_c, [&](int kind, int j, bool on) {
                 const bool use = on && ((act >> j) & 1u);
                 const double d = RHO * sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + RS * k + j], z);
-                const double y = L[Y.oY + RS * k + j] - d;
-                if (use) L[Y.oY + RS * k + j] = y;
+                const double y0 = L[Y.oY + RS * k + j], y = y0 - d;
+                L[Y.oY + RS * k + j] = use ? y : y0;             // unpredicated store (no exec mask per row)
                 upd = use ? fmax(upd, fabs(d)) : upd;
                 ym = use ? fmax(ym, fabs(y)) : ym;
             });
@@ -1500,8 +1500,9 @@ __device__ int eqp(Ctx& X, double scale) {
             const double rv = sp_dot(row_sp(kind, k < N, kb, vb), L[Y.oG + RS * k + j], z);
             const double y = L[Y.oY + RS * k + j];
             const bool in = (mask >> j) & 1u;
-            if (on) L[Y.oTLAM + RS * k + j] = in ? y : 0.0;
-            const bool flip = on && (in ? (y < -tl || fabs(rv) > tr) : rv < -tr);
+            if (on) L[Y.oTLAM + RS * k + j] = in ? y : 0.0;   // predicated: the terminal row shares a slot
+            // bitwise, not short-circuit: no branch per row
+            const bool flip = on & (in ? ((y < -tl) | (fabs(rv) > tr)) : (rv < -tr));
             mask = flip ? (mask ^ (1u << j)) : mask;
             bad += flip ? 1 : 0;
         });
