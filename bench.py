@@ -3,9 +3,11 @@
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--cpu-seconds S]
 
 A step = one launch of the batched solver over the config's ego batch (C2: trajectory1,
-N=20, B=4096 per GPU, seed 2; inputs resident in HBM).  Multi-GPU (torchrun, one rank per GPU,
-RCCL): each rank solves its own contiguous shard of the same ego stream (weak scaling, no
-data-path collective); timing = max over ranks.  Prints ONE JSON line on rank 0.
+N=20, B=4096 per GPU, seed 2; inputs resident in HBM).  Multi-GPU (one rank per GPU, started by
+torch.distributed.run or by `bench.py --gpus N` itself): each rank solves its own contiguous shard of the
+same ego stream (weak scaling, no data-path collective); the barrier, the max-over-ranks time and the
+one telemetry gather go through libmpcqp's RCCL communicator (shard.ShardComm, mpc_comm_* in
+include/mpcqp.h), not torch.distributed.  Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
@@ -86,7 +88,6 @@ def main():
 
     import numpy as np
     import torch
-    import torch.distributed as dist
     import __graft_entry__ as ge
     # one build per node (a no-op when the in-tree libraries are current); the other ranks load them
     # after the barrier below
@@ -100,13 +101,13 @@ def main():
             raise SystemExit("bench.py needs a GPU (the measurement runs libmpcqp's HIP kernels; --device cpu is "
                              "a test stand-in, not a measurement)")
         torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl" if gpu else "gloo", init_method="env://")
-        dist.barrier()
+    import shard
+    # the ranks' one collective (and the measurement's barrier / max over ranks): RCCL through libmpcqp's
+    # C ABI on GPU ranks (the unique id over a TCP rendezvous, no torch.distributed), gloo for the CPU stand-in
+    comm = shard.ShardComm.from_env(local if gpu else None)
+    comm.barrier()
     dev = torch.device("cuda", local) if gpu else torch.device("cpu")
     dev_index = local if gpu else -1
-
-    import shard
     cfg = W.CONFIGS[args.config]
     B = args.batch or cfg["B"] // max(1, cfg["gpus"])
     lo, hi = shard.shard_range(world * B, world, rank)      # weak scaling: B egos per GPU
@@ -142,8 +143,7 @@ def main():
     for _ in range(args.warmup):
         step()
     sync()
-    if world > 1:
-        dist.barrier()
+    comm.barrier()
     sync()
     if gpu:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
@@ -158,8 +158,7 @@ def main():
         else:
             tk.append(time.perf_counter())
     sync()
-    if world > 1:
-        dist.barrier()
+    comm.barrier()
     sync()
     wall = time.perf_counter() - t0
     if gpu:
@@ -167,17 +166,14 @@ def main():
     else:
         step_ms = np.diff(np.array(tk)) * 1e3
     gpu_s = float(step_ms.sum()) / 1e3
-    elapsed = max(wall, gpu_s)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = comm.max(max(wall, gpu_s))
 
     # the one collective: gather of per-rank solver telemetry (after the timed region)
     st_h = st.cpu().numpy() if gpu else host["status"]
     it_h = it.cpu().numpy() if gpu else host["iters"]
-    tel = shard.reduce_telemetry(shard.gather_telemetry(shard.telemetry(st_h, it_h),
-                                                        device=dev if world > 1 else None))
+    mat = shard.gather_telemetry(shard.telemetry(st_h, it_h), comm)
+    # rank 0 reports the whole job; the other ranks' figures below are their own shard's (not printed)
+    tel = shard.reduce_telemetry(mat if mat is not None else shard.gather_telemetry(shard.telemetry(st_h, it_h)))
     kmean = tel["mean_iters"]
     avg_launch_s = gpu_s / args.steps
     flops = algorithmic_flops(N, kmean) * B
@@ -201,9 +197,9 @@ def main():
 
     executed = executed_work(args.config)
     # closed-loop leg on every rank (its own ego shard), one gather to rank 0; after the headline timing
-    cl = closed_loop(args.config, args.closed_loop, N, dev_index, world, rank, dev) if args.closed_loop else None
+    cl = closed_loop(args.config, args.closed_loop, N, dev_index, comm) if args.closed_loop else None
     # offline-planner leg on every rank (its own chunk shard)
-    plan = plan_leg(args.plan_chunks, args.plan_steps, args.plan_route, world, rank, dev, args.cpu_seconds,
+    plan = plan_leg(args.plan_chunks, args.plan_steps, args.plan_route, comm, dev, args.cpu_seconds,
                     not args.no_cpu) if (args.plan_chunks and gpu) else None
     if plan is not None and args.plan_fleet > 0:
         try:
@@ -270,8 +266,7 @@ def main():
             out["cpu_backend"] = cpu_backend(wb, N, mo, min(args.cpu_seconds, 5.0))
             out["cpu_reference"] = cpu_reference(wb, N, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    comm.close()
 
 
 def launch_ranks(args):
@@ -406,7 +401,7 @@ def inflight(K, steps, wb, B, N, mo, X, U, dev, head):
                     "K streams; the headline value above is one batch at a time"}
 
 
-def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_egos=4):
+def closed_loop(config, B, N, device, comm, max_steps=3000, hist_egos=4):
     """B egos per GPU through run_simulation on the device (trajectory_tracking.py:377-443, mpc_closed_loop):
     starts near the reference start (s0 ~ U(0,2), v0 ~ U(0.5,2)) drawn for all world * B egos,
     each rank running its contiguous shard with the config's FSM preset, until every ego passed s_max - 1
@@ -414,12 +409,11 @@ def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_ego
     collective: a gather to rank 0 of every ego's check quantities and the FP32 histories of the first
     hist_egos egos of each shard (shard.py); rank 0 applies the restated verdicts to every ego."""
     import numpy as np
-    import torch
-    import torch.distributed as dist
     import mpcqp
     import shard
     import workloads as W
     import trajectory_tracking as TT
+    world, rank = comm.world, comm.rank
     cfg = W.CONFIGS[config]
     ld = W.loader(cfg["traj"])
     total = world * B
@@ -433,21 +427,15 @@ def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_ego
     fsm = TT.fsm_params(fsm_obj)
     p = mpcqp.default_params(N=N, sqp_iters=TT.SQP_ITERS)
     slv = mpcqp.Solver(ld.X_ref, ld.U_ref, p, device=device)
-    if world > 1:
-        dist.barrier()
+    comm.barrier()
     t0 = time.perf_counter()
     r = slv.closed_loop(x_init, fsm, max_steps=max_steps, s_max=ld.s_max)
-    dt = time.perf_counter() - t0
+    dt = comm.max(time.perf_counter() - t0)
     slv.close()
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
     tl_pos = fsm_obj.tl_pos if fsm_obj is not None else 0.0
     q = shard.closed_loop_quantities(r, lo, fsm_obj is not None, fsm_obj is not None, tl_pos)
     rows = -(-total // world)
-    payloads = shard.gather_closed_loop(shard.pack_closed_loop(q, r, rows, hist_egos, max_steps),
-                                        device=dev if world > 1 else None)
+    payloads = shard.gather_closed_loop(shard.pack_closed_loop(q, r, rows, hist_egos, max_steps), comm)
     if rank != 0:
         return None
     rep = shard.closed_loop_report(payloads, rows, hist_egos, max_steps, tuple(p.u_min), tuple(p.u_max), ld.s_max)
@@ -464,35 +452,43 @@ def closed_loop(config, B, N, device, world, rank, dev, max_steps=3000, hist_ego
 
 
 def executed_work(config):
-    """Executed FP64 work of this config's dominant kernel from the last PMC pass over it (rocprofv3 --pmc
+    """Executed FP64 work of this config's dominant kernel from the newest PMC pass over it (rocprofv3 --pmc
     SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64, SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES in their own
-    run: tools/gpu_f64_pmc.sh, summarised by tools/pmc_f64.py into profiles/r<NN>_pmc_f64_<config>.csv, the
-    newest round's file).
-    executed_frac = (2 FMA + MUL + ADD + TRANS) x 64 lanes / kernel time / 78.6 TF: an upper bound, since the
-    recursions issue under narrowed exec masks; valu_busy = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES."""
+    run: tools/gpu/pmc_f64.sh, joined with the kernel-stats CSV of the same command by tools/pmc_f64.py into
+    profiles/r<NN>_pmc_f64_<config>.csv).
+    The dominant kernel is the one with the largest total duration in that kernel-stats run (average x
+    launches); executed_frac = (2 FMA + MUL + ADD + TRANS) x 64 lanes / its average duration / 78.6 TF, an
+    upper bound since the recursions issue under narrowed exec masks; valu_busy = SQ_ACTIVE_INST_VALU /
+    SQ_WAVE_CYCLES.  Without a usable file the result says why ('unmeasured'), never a silent null."""
     import csv
+    prof = os.path.join(ROOT, "profiles")
     # the newest round's pass of this config (profiles/r<NN>_pmc_f64_<config>.csv)
-    cands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_pmc_f64_{config}.csv"))
+    cands = sorted(f for f in os.listdir(prof) if f.endswith(f"_pmc_f64_{config}.csv"))
     if not cands:
-        return {}
-    path = os.path.join(ROOT, "profiles", cands[-1])
+        return {"unmeasured": f"no profiles/r<NN>_pmc_f64_{config}.csv (no PMC pass over this config)"}
+    path = os.path.join(prof, cands[-1])
     rows = list(csv.DictReader(open(path)))
-    if not rows:
-        return {}
-    top = max(rows, key=lambda r: float(r.get("avg_duration_s") or 0.0))
     f = lambda r, k: float(r[k]) if r.get(k) not in (None, "") else None
+    timed = [r for r in rows if f(r, "avg_duration_s")]
+    if not timed:
+        return {"unmeasured": f"profiles/{cands[-1]} has no kernel durations (its PMC pass was not joined with a "
+                              "kernel-stats run)", "source": "profiles/" + cands[-1]}
+    total = lambda r: f(r, "total_duration_s") or f(r, "avg_duration_s") * float(r.get("launches") or 1)
+    top = max(timed, key=total)
     return {"executed_frac": f(top, "executed_frac_upper"), "valu_busy": f(top, "valu_busy"),
-            "kernel": top["kernel"], "source": "profiles/" + cands[-1],
+            "executed_TFLOPs": f(top, "executed_TFLOPs_upper"), "kernel": top["kernel"],
+            "source": "profiles/" + cands[-1], "stats_file": top.get("stats_file"),
             "per_kernel": {r["kernel"]: {"executed_TFLOPs_upper": f(r, "executed_TFLOPs_upper"),
                                          "executed_frac_upper": f(r, "executed_frac_upper"),
                                          "valu_busy": f(r, "valu_busy"), "fp64_insts": f(r, "fp64_insts"),
                                          "avg_duration_s": f(r, "avg_duration_s")} for r in rows},
-            "basis": "FP64 VALU instruction counts x 64 lanes / the kernel's average duration (upper bound: "
-                     "the Riccati recursions issue under exec masks of 5-10 lanes); valu_busy = "
-                     "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES"}
+            "basis": "dominant kernel = largest total duration in the kernel-stats run of the same command; FP64 "
+                     "VALU instruction counts x 64 lanes / its average duration (upper bound: the Riccati "
+                     "recursions issue under exec masks of 5-10 lanes); valu_busy = SQ_ACTIVE_INST_VALU / "
+                     "SQ_WAVE_CYCLES"}
 
 
-def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
+def plan_leg(B, steps, route_name, comm, dev, cpu_s, with_cpu):
     """Offline planner: B chunk NLPs per GPU (workloads.plan_batch_ref: 20 m chunks at random
     positions of the route, each with the reference's own horizon rule, 10% final chunks), solved on the device
     by libmpcplan, one launch per residency class of horizons (the chunks come sorted by N; a class's launch
@@ -502,10 +498,10 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
     GPU-vs-oracle agreement on the oracle's sample."""
     import numpy as np
     import torch
-    import torch.distributed as dist
     import mpcplan
     import shard
     import workloads as W
+    world, rank = comm.world, comm.rank
     r = W.plan_route(route_name)
     lo, hi = shard.shard_range(world * B, world, rank)
     wb = W.plan_batch_ref(r, hi - lo, seed=7, offset=lo)
@@ -561,8 +557,7 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
         join()
     step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    comm.barrier()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
     ev[0].record(stream)
@@ -572,15 +567,10 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(steps)])
-    el = max(wall, ms.sum() / 1e3)
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    el = comm.max(max(wall, ms.sum() / 1e3))
     # secondary: the same batches back to back with no join between them (a planning service fed
     # continuously), so one batch's slowest chunks overlap the next batch's launches on the other streams
-    if world > 1:
-        dist.barrier()
+    comm.barrier()
     ep = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     t1 = time.perf_counter()
     ep[0].record(stream)
@@ -590,11 +580,7 @@ def plan_leg(B, steps, route_name, world, rank, dev, cpu_s, with_cpu):
     join()
     ep[1].record(stream)
     torch.cuda.synchronize(dev)
-    pel = max(time.perf_counter() - t1, ep[0].elapsed_time(ep[1]) / 1e3)
-    if world > 1:
-        tt = torch.tensor([pel], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        pel = float(tt.item())
+    pel = comm.max(max(time.perf_counter() - t1, ep[0].elapsed_time(ep[1]) / 1e3))
     status, iters, sqp = (a.cpu().numpy() for a in o)
     out = None
     if rank == 0:
@@ -672,20 +658,16 @@ def plan_cpu_baseline(route, wb, budget_s, status, groups):
     on a bounded sample of the same chunks; and the GPU's agreement with it on that sample."""
     import numpy as np
     import plan_oracle as PO
-    hw = host_cores()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hw["affinity_cpus"]
+    hw, threads, share = cpu_threads()
     po = PO.PlanOracle(route)
     B = wb["x0"].shape[0]
-    n = min(B, 256)
+    n = min(B, max(256, 8 * threads))                    # >= 8 chunks per thread
     idx = np.linspace(0, B - 1, n).astype(int)           # spread over the horizons
     p = PO.default_params(N=int(wb["N"].max()))
     args = (wb["x0"][idx], wb["s_target"][idx], wb["is_final"][idx])
     ref = po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads)
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads)
-        done += n
-    dt = time.perf_counter() - t0
+    done, dt = _timed_rate(lambda: po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads), n, budget_s)
+    sdone, sdt = _timed_rate(lambda: po.solve_batch(p, *args, N=wb["N"][idx], num_threads=share), n, budget_s / 2)
     # GPU vs oracle on the sample: X of chunks both call converged (status 0 / 4)
     dmax, agree, both = 0.0, 0, 0
     for j, i in enumerate(idx):
@@ -698,9 +680,12 @@ def plan_cpu_baseline(route, wb, budget_s, status, groups):
             both += 1
             dmax = max(dmax, float(np.abs(xg - ref["X"][j][:nn + 1]).max()))
     base = {"value": done / dt, "unit": "chunks/s", "cores": threads, "kind": "port", "host": hw,
+            "scope": "all physical host cores (lscpu)",
             "sample": f"{n} chunks spread over the batch (all horizons), solved repeatedly for {dt:.1f} s by the "
                       f"planner oracle (oracle/plan_oracle.c, the same SQP and QP algorithm) with OpenMP, "
-                      f"{threads} threads"}
+                      f"{threads} threads",
+            "share": {"value": sdone / sdt, "unit": "chunks/s", "cores": share,
+                      "scope": "this GPU's share of the host (OMP_NUM_THREADS)"}}
     par = {"chunks": n, "status_agreement": agree / n, "both_converged": both, "max_abs_dX_both_converged": dmax}
     return base, par
 
@@ -729,54 +714,69 @@ def plan_cpu_reference(route, wb):
                       f"{procs} processes (oracle/plan_ref.py)"}
 
 
+def cpu_threads():
+    """Thread counts of the CPU legs: 'full' = every physical core of the host (lscpu), bounded by the CPUs this
+    process may run on, whatever OMP_NUM_THREADS the environment passes down (all physical host
+    cores of the GPU box); 'share' = this GPU's share of the host (OMP_NUM_THREADS, 16 on the GPU box), reported
+    beside it."""
+    hw = host_cores()
+    aff = hw["affinity_cpus"]
+    full = min(hw["physical_cores_lscpu"] or aff, aff)
+    share = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff, aff)
+    return hw, full, share
+
+
+def _timed_rate(fn, n, budget_s):
+    fn()                                              # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        fn()
+        done += n
+    return done, time.perf_counter() - t0
+
+
 def cpu_baseline(wb, N, mo, budget_s):
-    """The oracle's C restatement (same QP, same PDIP), OpenMP over the host CPUs this process may use, on
-    a bounded sample of the same egos.  kind = 'port' (the reference itself never travels to the GPU box)."""
+    """The oracle's C restatement (same QP, same PDIP), OpenMP over every physical core of the host, on the
+    whole per-GPU batch of the same egos, solved repeatedly for the budget; the same with this GPU's CPU share
+    as a secondary field.  kind = 'port' (the reference itself never travels to the GPU box)."""
     import oracle as O
     import workloads as W
     ld = W.loader(wb["traj"])
     orc = O.Oracle(ld.X_ref, ld.U_ref)
     p = O.default_params(N=N, max_obs=mo)
-    hw = host_cores()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hw["affinity_cpus"]
-    n = min(512, wb["x0"].shape[0])
-    sl = slice(0, n)
-    obs = None if wb["obs"] is None else wb["obs"][sl]
-    nob = None if wb["n_obs"] is None else wb["n_obs"][sl]
-    orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)        # warm
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        orc.solve_batch(p, wb["x0"][sl], obs, nob, num_threads=threads)
-        done += n
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "solves/s", "cores": threads, "kind": "port", "host": hw,
-            "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by the oracle's C PDIP "
-                      f"(oracle/mpc_oracle.c) with OpenMP, {threads} threads"}
+    hw, full, share = cpu_threads()
+    n = wb["x0"].shape[0]
+    out = {}
+    for tag, threads, budget in (("full", full, budget_s), ("share", share, budget_s / 2)):
+        done, dt = _timed_rate(lambda: orc.solve_batch(p, wb["x0"], wb["obs"], wb["n_obs"], num_threads=threads),
+                               n, budget)
+        out[tag] = {"value": done / dt, "unit": "solves/s", "cores": threads, "seconds": dt,
+                    "sample": f"the whole per-GPU batch ({n} egos), solved {done // n} times in {dt:.1f} s by the "
+                              f"oracle's C PDIP (oracle/mpc_oracle.c) with OpenMP, {threads} threads"}
+    return dict(out["full"], kind="port", host=hw, scope="all physical host cores (lscpu)",
+                share=dict(out["share"], scope="this GPU's share of the host (OMP_NUM_THREADS)"))
 
 
 def cpu_backend(wb, N, mo, budget_s):
-    """The product's own host backend (libmpcqp, mpc_create device = -1: csrc/cpu_backend.h) on the same bounded
-    sample and CPU share as cpu_baseline: what a user without a GPU gets (config 1's CPU path)."""
+    """The product's own host backend (libmpcqp, mpc_create device = -1: csrc/cpu_backend.h) on the whole per-GPU
+    batch, every physical core of the host and this GPU's share: what a user without a GPU gets (config 1's CPU
+    path)."""
     import mpcqp
     import workloads as W
     ld = W.loader(wb["traj"])
-    hw = host_cores()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hw["affinity_cpus"]
-    os.environ["MPC_CPU_THREADS"] = str(threads)
-    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo), device=-1)
-    n = min(512, wb["x0"].shape[0])
-    sl = slice(0, n)
-    obs = None if wb["obs"] is None else wb["obs"][sl]
-    nob = None if wb["n_obs"] is None else wb["n_obs"][sl]
-    slv.solve_batch(wb["x0"][sl], obs, nob)          # warm
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        slv.solve_batch(wb["x0"][sl], obs, nob)
-        done += n
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "solves/s", "cores": threads,
-            "sample": f"first {n} egos of the same batch, solved repeatedly for {dt:.1f} s by libmpcqp's host "
-                      f"backend (device = -1), {threads} threads"}
+    hw, full, share = cpu_threads()
+    n = wb["x0"].shape[0]
+    out = {}
+    for tag, threads in (("full", full), ("share", share)):
+        os.environ["MPC_CPU_THREADS"] = str(threads)
+        slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo), device=-1)
+        done, dt = _timed_rate(lambda: slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"]), n, budget_s / 2)
+        slv.close()
+        out[tag] = {"value": done / dt, "unit": "solves/s", "cores": threads,
+                    "sample": f"the whole per-GPU batch ({n} egos), solved {done // n} times in {dt:.1f} s by "
+                              f"libmpcqp's host backend (device = -1), {threads} threads"}
+    return dict(out["full"], scope="all physical host cores (lscpu)",
+                share=dict(out["share"], scope="this GPU's share of the host (OMP_NUM_THREADS)"))
 
 
 def host_cores():

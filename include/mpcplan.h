@@ -97,8 +97,12 @@ int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const 
  * horizon N and Nmax < params N is PLAN_E_ARG (rows past a chunk's horizon are written as zero).  A chunk
  * whose N[b] lies outside [1, Nmax] is not solved (zero plan, status PLAN_NUMERICAL).  The kernel needs no
  * scratch memory: each chunk's working set lives in LDS (about 2.1 KB per stage, sized for Nmax; Nmax is
- * limited by the device's LDS per workgroup, 64 at 160 KB), so the call allocates nothing and can be
- * captured into a graph. */
+ * limited by the device's LDS per workgroup, 64 at 160 KB).  Batches of 128 .. 2^17 chunks are dispatched
+ * longest first through a small per-context pool of order buffers (at most 8, allocated by the first eager
+ * calls that need them, freed by plan_destroy); each buffer is reused only after the chunk kernel that last
+ * read it has finished (an event, so eager calls on any streams stay correct).  A call made while `stream` is
+ * being captured into a HIP graph uses no pool buffer (index order, the same results) and allocates nothing,
+ * so graphs and eager calls never share a buffer. */
 int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const double* x0,
                              const double* s_target, const int* is_final, double* X, double* U, double* S,
                              int* status, int* iters, int* sqp, void* stream);

@@ -23,6 +23,8 @@
 #ifndef MPCQP_H
 #define MPCQP_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -49,6 +51,7 @@ extern "C" {
 #define MPC_E_DEVICE (-2)
 #define MPC_E_ALLOC (-3)
 #define MPC_E_LAUNCH (-4)
+#define MPC_E_COMM (-5)       /* RCCL missing or a collective failed (mpc_comm_*, mpc_gather*)   */
 
 /* Mirrors TrajectoryTracker.__init__ (trajectory_tracking.py:17-47) plus solver knobs.
  * Field names follow the reference attributes.  mpc_default_params() fills the reference values. */
@@ -178,6 +181,33 @@ void mpc_default_fsm(mpc_fsm* f);
 int mpc_closed_loop(mpc_ctx* c, int B, const double* x_init, const mpc_fsm* fsm, int max_steps, double s_stop,
                     double* hist_x, double* hist_u, double* hist_obs_s, int* hist_tl, int* hist_status,
                     int* n_steps, double* step_ms);
+
+/* ---- Multi-GPU: ego shards, one gather ----------------------------------------------------
+ * Every ego is independent; a batch splits into contiguous per-rank shards (one process per GPU) with no
+ * per-step exchange.  The one collective returns what the reference's run_simulation returns
+ * (trajectory_tracking.py:443: the closed-loop histories) to rank 0: ncclGather (RCCL over xGMI,
+ * rccl.h:745) of a fixed-size payload per rank.  RCCL is loaded (dlopen librccl.so.1) by the first
+ * mpc_comm_unique_id / mpc_comm_create; without it they fail with MPC_E_COMM.
+ *   - rank 0 calls mpc_comm_unique_id and hands the MPC_COMM_UID_BYTES bytes to every rank out of band (the
+ *     package's shard.py uses a TCP rendezvous on MASTER_ADDR); every rank then calls mpc_comm_create
+ *     (collective: it returns once all nranks ranks joined);
+ *   - mpc_gather: device buffers, asynchronous on `stream` (hipStream_t, 0 = null stream): rank i's `bytes`
+ *     land at recv + i*bytes on the root (recv holds nranks*bytes there; may be NULL elsewhere);
+ *   - mpc_gather_host: the same from host buffers, staged through the communicator's device buffer on its
+ *     own stream, synchronous (returns when the root's recv is filled);
+ *   - mpc_comm_allreduce_max: in-place max of one double over all ranks (the measurement's max-over-ranks
+ *     time), synchronous; mpc_comm_barrier: returns on every rank once all ranks entered it;
+ *   - one communicator per process and device; not re-entrant. */
+#define MPC_COMM_UID_BYTES 128
+typedef struct mpc_comm mpc_comm;
+int mpc_comm_unique_id(char* uid /* [MPC_COMM_UID_BYTES] */);
+int mpc_comm_create(const char* uid, int nranks, int rank, int device, mpc_comm** out);
+int mpc_comm_info(const mpc_comm* c, int* nranks, int* rank, int* device);
+int mpc_gather(mpc_comm* c, const void* send, size_t bytes, void* recv, int root, void* stream);
+int mpc_gather_host(mpc_comm* c, const void* send, size_t bytes, void* recv, int root);
+int mpc_comm_allreduce_max(mpc_comm* c, double* value);
+int mpc_comm_barrier(mpc_comm* c);
+void mpc_comm_destroy(mpc_comm* c);
 
 /* Thread-local description of the last API error on this thread. */
 const char* mpc_last_error(void);

@@ -2952,3 +2952,6 @@ extern "C" int mpc_lookup(mpc_ctx* c, int n, const double* s, double* out_state,
     HIPCHK(hipStreamSynchronize(st), MPC_E_DEVICE);
     return MPC_SUCCESS;
 }
+
+// multi-GPU: the ego-shard communicator (RCCL gather behind the C ABI)
+#include "comm.h"

@@ -54,27 +54,59 @@ struct plan_ctx {
     // host-entry staging
     void* io;
     size_t io_bytes;
-    // longest-first dispatch (plan_order_*_kernel): one buffer per stream the context launches on (2 *
-    // ORDER_BUCKETS counters, then bucket[cap], order[cap]), so calls on different streams never share one;
-    // allocated on a stream's first eager call (a call being captured into a graph without a buffer for its
-    // stream, or a batch above cap_order, runs in index order: same results)
-    std::vector<std::pair<void*, int*>> order_bufs;
+    // longest-first dispatch (plan_order_*_kernel): a small pool of buffers (2 * ORDER_BUCKETS counters, then
+    // bucket[cap], order[cap]), each remembering the stream it last served and an event recorded after its last
+    // chunk kernel.  A call prefers its stream's buffer, else a new one (up to ORDER_POOL), else the least
+    // recently used; before using a buffer it waits for that buffer's event, so a buffer is never rewritten
+    // while an earlier plan_chunk_kernel still reads its order[] (whatever stream that ran on, and whether or
+    // not a new stream reuses a destroyed stream's address).  Concurrent launches on distinct streams keep
+    // distinct buffers.  A call on a stream that is being captured into a graph never uses the pool (index
+    // order, same results): a graph must not replay order kernels against a buffer shared with eager calls.
+    struct OrderBuf {
+        int* ptr;
+        hipEvent_t done;
+        void* stream;
+        unsigned long long last_use;
+        bool used;
+    };
+    std::vector<OrderBuf> order_bufs;
+    unsigned long long order_clock;
     std::mutex order_mu;
     int cap_order;
     bool order_on;
 };
 
-// the stream's order buffer, or nullptr (capturing without one, or allocation failure: index order)
-static int* order_buffer(plan_ctx* c, void* stream) {
-    std::lock_guard<std::mutex> g(c->order_mu);
-    for (auto& e : c->order_bufs)
-        if (e.first == stream) return e.second;
+#define ORDER_POOL 8
+
+// the buffer this call may use (its event already waited on by `stream`), or nullptr: index order (the stream
+// is being captured, or an allocation failed)
+static plan_ctx::OrderBuf* order_buffer(plan_ctx* c, void* stream) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    int* buf = nullptr;
-    if (hipMalloc(&buf, sizeof(int) * (2 * (size_t)ORDER_BUCKETS + 2 * (size_t)c->cap_order)) != hipSuccess) return nullptr;
-    c->order_bufs.emplace_back(stream, buf);
-    return buf;
+    std::lock_guard<std::mutex> g(c->order_mu);
+    plan_ctx::OrderBuf* b = nullptr;
+    for (auto& e : c->order_bufs)
+        if (e.stream == stream) b = &e;
+    if (!b && c->order_bufs.size() < ORDER_POOL) {
+        plan_ctx::OrderBuf e{};
+        if (hipMalloc(&e.ptr, sizeof(int) * (2 * (size_t)ORDER_BUCKETS + 2 * (size_t)c->cap_order)) != hipSuccess)
+            return nullptr;
+        if (hipEventCreateWithFlags(&e.done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipFree(e.ptr);
+            return nullptr;
+        }
+        c->order_bufs.push_back(e);
+        b = &c->order_bufs.back();
+    }
+    if (!b) {
+        b = &c->order_bufs[0];
+        for (auto& e : c->order_bufs)
+            if (e.last_use < b->last_use) b = &e;
+    }
+    if (b->used && hipStreamWaitEvent((hipStream_t)stream, b->done, 0) != hipSuccess) return nullptr;
+    b->stream = stream;
+    b->last_use = ++c->order_clock;
+    return b;
 }
 
 static int check_params(const plan_params* p) {
@@ -165,6 +197,7 @@ int plan_create(const double* s, int M, const double* cx, const double* cy, cons
     c->R.M = M;
     c->R.s_total = s[M - 1];
     c->cap_order = 1 << 17;
+    c->order_bufs.reserve(ORDER_POOL);      // never reallocated: buffer pointers stay valid
     const char* oe = std::getenv("PLAN_ORDER");        // PLAN_ORDER=0: index order (A/B)
     c->order_on = !(oe && oe[0] == '0');
     *out = c;
@@ -184,7 +217,10 @@ void plan_destroy(plan_ctx* c) {
     (void)hipDeviceSynchronize();
     if (c->d_route) (void)hipFree(c->d_route);
     if (c->io) (void)hipFree(c->io);
-    for (auto& e : c->order_bufs) (void)hipFree(e.second);
+    for (auto& e : c->order_bufs) {
+        (void)hipFree(e.ptr);
+        (void)hipEventDestroy(e.done);
+    }
     delete c;
 }
 
@@ -219,9 +255,9 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
     a.x0 = x0;
     a.st = s_target;
     a.order = nullptr;
-    int* obuf = (c->order_on && B >= 2 * WAVE && B <= c->cap_order) ? order_buffer(c, stream) : nullptr;
-    if (obuf) {
-        int* cnt = obuf;
+    plan_ctx::OrderBuf* ob = (c->order_on && B >= 2 * WAVE && B <= c->cap_order) ? order_buffer(c, stream) : nullptr;
+    if (ob) {
+        int* cnt = ob->ptr;
         int* bucket = cnt + 2 * ORDER_BUCKETS;
         int* order = bucket + c->cap_order;
         const int nb = (B + 255) / 256;
@@ -245,6 +281,13 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
     hipLaunchKernelGGL(plan_chunk_kernel, dim3(B), dim3(WAVE), lds, (hipStream_t)stream, a);
     if (hipError_t e = hipGetLastError(); e != hipSuccess)
         return fail(PLAN_E_LAUNCH, std::string("plan kernel launch failed: ") + hipGetErrorString(e));
+    if (ob) {
+        // the buffer is free again once this kernel has read its order[]
+        std::lock_guard<std::mutex> g(c->order_mu);
+        if (hipEventRecord(ob->done, (hipStream_t)stream) != hipSuccess)
+            return fail(PLAN_E_DEVICE, "order buffer event record failed");
+        ob->used = true;
+    }
     return PLAN_SUCCESS;
 }
 

@@ -53,7 +53,10 @@ class MpcError(RuntimeError):
 
 EXPORTS = ["mpc_default_params", "mpc_create", "mpc_solve_batch", "mpc_solve_batch_device", "mpc_lookup",
            "mpc_set_params", "mpc_get_params", "mpc_last_error", "mpc_version", "mpc_destroy", "mpc_default_fsm",
-           "mpc_closed_loop", "mpc_global_pose", "mpc_read_trajectory_json", "mpc_create_from_json"]
+           "mpc_closed_loop", "mpc_global_pose", "mpc_read_trajectory_json", "mpc_create_from_json",
+           "mpc_comm_unique_id", "mpc_comm_create", "mpc_comm_info", "mpc_gather", "mpc_gather_host",
+           "mpc_comm_allreduce_max", "mpc_comm_barrier", "mpc_comm_destroy"]
+COMM_UID_BYTES = 128
 
 _lib = None
 
@@ -93,6 +96,21 @@ def lib():
     L.mpc_closed_loop.restype = C.c_int
     L.mpc_closed_loop.argtypes = [C.c_void_p, C.c_int, _dp, C.POINTER(MpcFsm), C.c_int, C.c_double, _dp, _dp, _dp,
                                   _ip, _ip, _ip, _dp]
+    L.mpc_comm_unique_id.restype = C.c_int
+    L.mpc_comm_unique_id.argtypes = [C.c_char_p]
+    L.mpc_comm_create.restype = C.c_int
+    L.mpc_comm_create.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.mpc_comm_info.restype = C.c_int
+    L.mpc_comm_info.argtypes = [C.c_void_p, _ip, _ip, _ip]
+    L.mpc_gather.restype = C.c_int
+    L.mpc_gather.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int, C.c_void_p]
+    L.mpc_gather_host.restype = C.c_int
+    L.mpc_gather_host.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_int]
+    L.mpc_comm_allreduce_max.restype = C.c_int
+    L.mpc_comm_allreduce_max.argtypes = [C.c_void_p, _dp]
+    L.mpc_comm_barrier.restype = C.c_int
+    L.mpc_comm_barrier.argtypes = [C.c_void_p]
+    L.mpc_comm_destroy.argtypes = [C.c_void_p]
     _lib = L
     return L
 
@@ -238,3 +256,55 @@ class Solver:
         st = np.empty((s.size, 5)); ct = np.empty((s.size, 2))
         _check(lib().mpc_lookup(self.h, s.size, _p(s), _p(st), _p(ct)), "mpc_lookup")
         return st, ct
+
+
+def comm_unique_id():
+    """mpc_comm_unique_id: the RCCL unique id (COMM_UID_BYTES bytes) that rank 0 hands to every rank."""
+    buf = C.create_string_buffer(COMM_UID_BYTES)
+    _check(lib().mpc_comm_unique_id(buf), "mpc_comm_unique_id")
+    return buf.raw
+
+
+class Comm:
+    """One libmpcqp ego-shard communicator (mpc_comm_*: RCCL over xGMI behind the C ABI, include/mpcqp.h).
+    Collective construction: every rank of `nranks` calls it with rank 0's unique id."""
+
+    def __init__(self, uid, nranks, rank, device):
+        if len(uid) != COMM_UID_BYTES:
+            raise ValueError(f"uid must be {COMM_UID_BYTES} bytes")
+        h = C.c_void_p()
+        _check(lib().mpc_comm_create(uid, int(nranks), int(rank), int(device), C.byref(h)), "mpc_comm_create")
+        self.h, self.nranks, self.rank, self.device = h, int(nranks), int(rank), int(device)
+
+    def gather(self, payload, root=0):
+        """mpc_gather_host of a uint8 payload (the same size on every rank): the list of every rank's payload on
+        the root, None elsewhere."""
+        buf = np.ascontiguousarray(payload, np.uint8).ravel()
+        out = np.empty(buf.size * self.nranks, np.uint8) if self.rank == root else None
+        _check(lib().mpc_gather_host(self.h, buf.ctypes.data, buf.size, None if out is None else out.ctypes.data,
+                                     int(root)), "mpc_gather_host")
+        return None if out is None else [out[i * buf.size:(i + 1) * buf.size] for i in range(self.nranks)]
+
+    def gather_device(self, send_ptr, nbytes, recv_ptr, root=0, stream=0):
+        """mpc_gather on device buffers (raw addresses), asynchronous on `stream`."""
+        _check(lib().mpc_gather(self.h, send_ptr, int(nbytes), recv_ptr, int(root), C.c_void_p(stream)),
+               "mpc_gather")
+
+    def allreduce_max(self, x):
+        v = C.c_double(float(x))
+        _check(lib().mpc_comm_allreduce_max(self.h, C.byref(v)), "mpc_comm_allreduce_max")
+        return v.value
+
+    def barrier(self):
+        _check(lib().mpc_comm_barrier(self.h), "mpc_comm_barrier")
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            lib().mpc_comm_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -12,6 +12,7 @@ loop (:419-559) and ends with reference_trajectory_check (:557).  Route acquisit
 GraphHopper over HTTP) is out of scope: routes.py builds the route from local way-points.
 """
 import math
+import threading
 import time
 
 import numpy as np
@@ -82,10 +83,9 @@ class TrajectoryOptimizer:
         return p
 
     def planner(self, route, v_min=0.0):
-        """The route's shared context (planner_for), with this optimizer's parameters."""
-        pl = planner_for(route, self.device)
-        pl.set_params(self.params(v_min))
-        return pl
+        """A context of its own for `route` with this optimizer's parameters (the caller closes it).  optimize()
+        itself uses the route's shared context (planner_for) under the module lock instead."""
+        return mpcplan.Planner(route, self.params(v_min), device=self.device)
 
     def optimize(self, x0, s_target, s_total, k_ref_fun, v_min_fun, v_max_fun, is_final_chunk):
         """:351-390 — returns (X [N+1,5], U [N,2], S [N]); the chunk's status is left in self.last_status.
@@ -103,8 +103,11 @@ class TrajectoryOptimizer:
         if not (vs[0] == vs[1] == vs[2]):
             raise TypeError("v_min_fun must be constant over the chunk (the device rows take one v_min; the "
                             f"reference's is 0): got {vs} at s = x0, midpoint, s_target")
-        r = self.planner(route, vs[0]).solve_chunks(np.asarray(x0, np.float64)[None], float(s_target),
-                                                    int(bool(is_final_chunk)), int(self.N))
+        with _LOCK:
+            pl = planner_for(route, self.device)
+            pl.set_params(self.params(vs[0]))
+            r = pl.solve_chunks(np.asarray(x0, np.float64)[None], float(s_target), int(bool(is_final_chunk)),
+                                int(self.N))
         self.last_status = int(r["status"][0])
         return r["X"][0], r["U"][0], r["S"][0]
 
@@ -158,32 +161,74 @@ def route_from_functions(k_ref_fun, v_max_fun):
     hit = _ROUTES.get(key)
     # the objects are the key while they live; a hit must still hold the very same objects
     if hit is not None and hit._s_to_t is s_to_t[0] and hit._vint is vint[0] and hit.spline[0] is spl[0][0]:
-        return hit
-    r = routes.Route.from_reference_functions(s_to_t[0], spl[0], vint[0], name="reference-closures")
-    if len(_ROUTES) >= MAX_CACHED_ROUTES:
-        _ROUTES.pop(next(iter(_ROUTES)))
-    _ROUTES[key] = r
+        r = hit
+        _ROUTES[key] = _ROUTES.pop(key)                 # most recently used last
+    else:
+        r = routes.Route.from_reference_functions(s_to_t[0], spl[0], vint[0], name="reference-closures")
+        while len(_ROUTES) >= MAX_CACHED_ROUTES:
+            _ROUTES.pop(next(iter(_ROUTES)))
+        _ROUTES[key] = r
+    _verify_closures(k_ref_fun, v_max_fun, r)
     return r
+
+
+_VERIFIED = {}        # (id(k_ref_fun), id(v_max_fun)) -> (k_ref_fun, v_max_fun, route) checked against the route
+
+
+def _verify_closures(k_ref_fun, v_max_fun, route, samples=96):
+    """The recovered route replaces the caller's closures on the device, so they must compute what the route
+    computes: k_ref_fun / v_max_fun are evaluated at up to `samples` knots and interval midpoints spread over
+    the route and compared bit for bit with the route's own k_ref_fun / v_max_fun (a closure over the same
+    objects that returns something else -- heading, a scaled curvature, a modified limit -- raises
+    TypeError).  Checked once per pair of function objects."""
+    key = (id(k_ref_fun), id(v_max_fun))
+    got = _VERIFIED.get(key)
+    if got is not None and got[0] is k_ref_fun and got[1] is v_max_fun and got[2] is route:
+        return
+    s = np.asarray(route.s, np.float64)
+    idx = np.unique(np.linspace(0, s.size - 2, min(samples // 2, s.size - 1)).astype(int))
+    pts = np.concatenate([s[idx], 0.5 * (s[idx] + s[idx + 1]), s[-1:]])
+    same = lambda a, b: (a == b) or (np.isnan(a) and np.isnan(b))
+    for x in pts:
+        x = float(x)
+        if not same(float(k_ref_fun(x)), route.k_ref_fun(x)):
+            raise TypeError(f"k_ref_fun({x}) = {float(k_ref_fun(x))!r} differs from the curvature of the route it "
+                            f"closes over ({route.k_ref_fun(x)!r}): the device evaluates the reference's curvature "
+                            "(trajectory_planning.py:445-459) only")
+        if not same(float(v_max_fun(x)), route.v_max_fun(x)):
+            raise TypeError(f"v_max_fun({x}) = {float(v_max_fun(x))!r} differs from the route's speed limit "
+                            f"({route.v_max_fun(x)!r}): the device evaluates the reference's limit "
+                            "(trajectory_planning.py:470-473) only")
+    while len(_VERIFIED) >= MAX_CACHED_ROUTES:
+        _VERIFIED.pop(next(iter(_VERIFIED)))
+    _VERIFIED[key] = (k_ref_fun, v_max_fun, route)
+
+
+_LOCK = threading.RLock()     # planner_for + set_params + solve of the shared contexts (not re-entrant in C)
 
 
 def planner_for(route, device=0):
     """One libmpcplan context per distinct route (content hash of its device arrays) and device, shared by every
     TrajectoryOptimizer: the reference's per-chunk optimizers (:517) reuse it, so a route is uploaded once.
-    At most MAX_CACHED_ROUTES contexts are kept (the oldest is closed first); release_planners() closes all."""
+    At most MAX_CACHED_ROUTES contexts are kept, least recently used closed first; release_planners() closes
+    all.  The contexts are shared and a C context is not re-entrant: callers hold _LOCK from here through
+    their solve (TrajectoryOptimizer.optimize does)."""
     key = (route.content_key(), int(device))
-    pl = _PLANNERS.get(key)
-    if pl is None:
-        if len(_PLANNERS) >= MAX_CACHED_ROUTES:
-            _PLANNERS.pop(next(iter(_PLANNERS))).close()
-        pl = mpcplan.Planner(route, device=device)
-        _PLANNERS[key] = pl
-    return pl
+    with _LOCK:
+        pl = _PLANNERS.pop(key, None)
+        if pl is None:
+            while len(_PLANNERS) >= MAX_CACHED_ROUTES:
+                _PLANNERS.pop(next(iter(_PLANNERS))).close()
+            pl = mpcplan.Planner(route, device=device)
+        _PLANNERS[key] = pl                              # most recently used last
+        return pl
 
 
 def release_planners():
     """Close every cached planner context."""
-    while _PLANNERS:
-        _PLANNERS.popitem()[1].close()
+    with _LOCK:
+        while _PLANNERS:
+            _PLANNERS.popitem()[1].close()
 
 
 def optimize_full_trajectory(route, max_chunk_size=20, max_chunks=10000, device=0, verbose=False, check=True,

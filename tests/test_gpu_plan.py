@@ -290,6 +290,85 @@ def test_longest_first_order_changes_nothing(env, monkeypatch):
     ordered.close()
 
 
+def test_graph_capture_after_eager_warmup(env):
+    """an eager call on a stream (which takes a longest-first order buffer), then the same call
+    captured into a HIP graph on that stream and replayed, interleaved with eager calls on the same context:
+    the captured call must not use the pool (index order), so replays and eager calls never rewrite each
+    other's order[]; every replay and every eager call equals the index-order result bit for bit."""
+    import torch
+    mpcplan, PO, W = env
+    r = W.plan_route("traj3")
+    B = 1024
+    wb = W.plan_batch(r, 14, B, seed=41, final_frac=0.1)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    x0, st, fin = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32)
+    ref = mpcplan.Planner(r, mpcplan.default_params(N=14)).solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=14))
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+
+    def outputs():
+        return torch.empty((B, 15, 5), dtype=torch.float64, device=dev), [torch.empty(B, dtype=torch.int32, device=dev)
+                                                                          for _ in range(3)]
+
+    def call(X, o, stream):
+        pl.solve_chunks_device(B, 14, 0, x0.data_ptr(), st.data_ptr(), fin.data_ptr(), X.data_ptr(), 0, 0,
+                               *[a.data_ptr() for a in o], stream=stream)
+
+    def check(X, o, what):
+        assert np.array_equal(X.cpu().numpy(), ref["X"]), what
+        assert np.array_equal(o[0].cpu().numpy(), ref["status"]) and np.array_equal(o[2].cpu().numpy(), ref["sqp"]), what
+
+    Xe, oe = outputs()
+    with torch.cuda.stream(side):
+        call(Xe, oe, side.cuda_stream)                    # eager warm-up: the side stream gets a pool buffer
+    torch.cuda.synchronize(dev)
+    check(Xe, oe, "eager")
+    Xg, og = outputs()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        call(Xg, og, torch.cuda.current_stream(dev).cuda_stream)
+    for k in range(3):
+        Xg.zero_()
+        g.replay()
+        Xe2, oe2 = outputs()
+        call(Xe2, oe2, side.cuda_stream)                  # an eager call right behind the replay
+        torch.cuda.synchronize(dev)
+        check(Xg, og, f"replay {k}")
+        check(Xe2, oe2, f"eager after replay {k}")
+    pl.close()
+
+
+def test_order_pool_reuse_across_many_streams(env):
+    """More concurrent streams than the pool holds (8): buffers are reused least recently used, each only after
+    the kernel that last read it has finished; every launch equals the index-order result."""
+    import torch
+    mpcplan, PO, W = env
+    r = W.plan_route("traj3")
+    B = 512
+    wb = W.plan_batch(r, 12, B, seed=43, final_frac=0.1)
+    dev = torch.device("cuda", 0)
+    t = lambda a, dt=torch.float64: torch.as_tensor(a, dtype=dt, device=dev).contiguous()
+    x0, st, fin = t(wb["x0"]), t(wb["s_target"]), t(wb["is_final"], torch.int32)
+    ref = mpcplan.Planner(r, mpcplan.default_params(N=12)).solve_chunks(wb["x0"], wb["s_target"], wb["is_final"])
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=12))
+    streams = [torch.cuda.Stream(dev) for _ in range(12)]
+    outs = []
+    for rep in range(2):
+        for s in streams:
+            s.wait_stream(torch.cuda.current_stream(dev))
+            X = torch.empty((B, 13, 5), dtype=torch.float64, device=dev)
+            o = [torch.empty(B, dtype=torch.int32, device=dev) for _ in range(3)]
+            pl.solve_chunks_device(B, 12, 0, x0.data_ptr(), st.data_ptr(), fin.data_ptr(), X.data_ptr(), 0, 0,
+                                   *[a.data_ptr() for a in o], stream=s.cuda_stream)
+            outs.append((X, o))
+    torch.cuda.synchronize(dev)
+    for X, o in outs:
+        assert np.array_equal(X.cpu().numpy(), ref["X"]) and np.array_equal(o[0].cpu().numpy(), ref["status"])
+    pl.close()
+
+
 def test_residency_groups(env):
     """plan_chunks_per_cu is non-increasing in Nmax and at least 1 up to PLAN_MAX_N; Planner.horizon_groups
     puts each horizon in one launch whose residency equals its own launch's; the grouped launches (per-chunk N,

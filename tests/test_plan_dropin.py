@@ -109,6 +109,33 @@ def test_route_recovery_rejects_other_callables(mods):
         TP.route_from_functions(r.k_ref_fun, W.plan_route("synth2").v_max_fun)
 
 
+def test_closures_computing_something_else_are_refused(mods):
+    """closures over the very objects route_from_functions recovers the route from, but returning
+    something else (a scaled curvature, a modified limit), would be replaced by the device's curvature / limit
+    and solve a different NLP: they are evaluated against the recovered route and raise TypeError."""
+    routes, TP, W = mods
+    r = W.plan_route("traj1")
+    pts, spline, lim = reference_inputs(r)
+    k_ref_fun, _, v_max_fun, _, _ = reference_closures(pts, spline, lim)
+    cells = TP._closure(k_ref_fun)
+    s_to_t, sp = cells["s_to_t"], cells["reference_path_spline"]
+    vint = TP._closure(v_max_fun)["v_max_interpolator"]
+
+    def k_scaled(s):
+        t = float(s_to_t(s))
+        x_spline, y_spline = sp
+        return 2.0 * float((x_spline(t, 1) * y_spline(t, 2) - y_spline(t, 1) * x_spline(t, 2)) /
+                           ((x_spline(t, 1) ** 2 + y_spline(t, 1) ** 2) ** 1.5 + 1e-9))
+
+    def v_capped(s):
+        return min(float(vint(s)), 5.0)
+    with pytest.raises(TypeError, match="k_ref_fun"):
+        TP.route_from_functions(k_scaled, v_max_fun)
+    with pytest.raises(TypeError, match="v_max_fun"):
+        TP.route_from_functions(k_ref_fun, v_capped)
+    assert TP.route_from_functions(k_ref_fun, v_max_fun).content_key() == r.content_key()
+
+
 def test_nonconstant_v_min_is_refused(mods):
     """The device rows take one v_min per chunk; the reference calls v_min_fun(s_k) per stage (:259), so a
     v_min_fun that varies over the chunk raises instead of solving a different NLP (checked before any device

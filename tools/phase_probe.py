@@ -10,6 +10,10 @@ import numpy as np
 import mpcqp
 import workloads as W
 
+import __graft_entry__ as _ge
+# the diagnostic twin must be built from the current sources (build() rebuilds it unless its .srchash matches),
+# so the phase numbers never describe an older kernel
+_ge.build(prof=True)
 mpcqp.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcqp_prof.so")
 L = mpcqp.lib()
 L.mpc_debug_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]

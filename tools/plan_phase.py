@@ -10,11 +10,15 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "safe-autonomous-driving-mpc_amd"), ROOT]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "safe-autonomous-driving-mpc_amd")]
 import numpy as np
 
 import mpcplan
 
+import __graft_entry__ as _ge
+# the diagnostic twin must be built from the current sources (build() rebuilds it unless its .srchash matches),
+# so the phase numbers never describe an older kernel
+_ge.build(prof=True)
 mpcplan.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcplan_prof.so")
 import workloads as W
 

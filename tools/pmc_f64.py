@@ -7,11 +7,13 @@ Per launch of each kernel (mode XO / IPM / FULL / ONE, template <OBS, G, MODE, N
   count is lower;
 - VALU-busy: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (both in quad-cycles, MI355X_MICROARCH.md), the fraction
   of resident-wave time spent issuing VALU instructions.
-With a kernel-stats CSV (rocprofv3 --stats, same config) the flops are divided by the kernel's average
-duration to give executed TFLOP/s and its fraction of the 78.6 TF FP64 peak.
+The kernel-stats CSV of the same command (rocprofv3 --kernel-trace --stats, its own run) is required: the
+flops are divided by each kernel's average duration to give executed TFLOP/s and its fraction of the 78.6 TF
+FP64 peak, and every counted kernel must find its duration there (the script stops otherwise, so a summary
+without durations cannot be written).
 
-  python tools/pmc_f64.py C2 [stats.csv]   ->  gpurun_out/pmc_f64_C2.csv and one JSON line per kernel
-  python tools/pmc_f64.py plan [stats.csv] ->  the planner kernel (tools/gpu_plan_pmc.sh)
+  python tools/pmc_f64.py C2 STATS.csv     ->  gpurun_out/pmc_f64_C2.csv and one JSON line per kernel
+  python tools/pmc_f64.py plan STATS.csv   ->  the planner kernel (tools/gpu/plan_pmc_f64.sh)
 """
 import csv
 import glob
@@ -58,16 +60,23 @@ def load_stats(path):
     for row in csv.DictReader(open(path)):
         k = kernel_key(row.get("Name", ""))
         if k is not None:
-            out[k] = float(row["AverageNs"]) * 1e-9
+            out[k] = (float(row["AverageNs"]) * 1e-9, float(row["TotalDurationNs"]) * 1e-9)
     return out
 
 
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
-    stats = load_stats(sys.argv[2] if len(sys.argv) > 2 else None)
+    if len(sys.argv) < 3:
+        raise SystemExit("usage: pmc_f64.py CONFIG STATS.csv (the kernel-stats CSV of the same command)")
+    stats = load_stats(sys.argv[2])
+    if not stats:
+        raise SystemExit(f"no solver kernel in {sys.argv[2]}")
     per = load_counters(os.path.join(ROOT, "gpurun_out", f"pmc_f64_{cfg}"))
     if not per:
         raise SystemExit("no counter rows found")
+    missing = sorted(set(per) - set(stats))
+    if missing:
+        raise SystemExit(f"no kernel-stats duration for {missing} in {sys.argv[2]}")
     rows = []
     for k, disp in sorted(per.items()):
         n = len(disp)
@@ -79,10 +88,10 @@ def main():
         r = {"config": cfg, "kernel": k, "launches": n, **{c: avg[c] for c in CTRS},
              "fp64_insts": insts, "fp64_flops_upper": flops_ub,
              "valu_busy": avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"] if avg["SQ_WAVE_CYCLES"] else None}
-        if k in stats:
-            r["avg_duration_s"] = stats[k]
-            r["executed_TFLOPs_upper"] = flops_ub / stats[k] / 1e12
-            r["executed_frac_upper"] = r["executed_TFLOPs_upper"] / PEAK
+        r["avg_duration_s"], r["total_duration_s"] = stats[k]
+        r["stats_file"] = os.path.basename(sys.argv[2])
+        r["executed_TFLOPs_upper"] = flops_ub / stats[k][0] / 1e12
+        r["executed_frac_upper"] = r["executed_TFLOPs_upper"] / PEAK
         rows.append(r)
     out = os.path.join(ROOT, "gpurun_out", f"pmc_f64_{cfg}.csv")
     keys = sorted({k for r in rows for k in r}, key=lambda x: (x not in ("config", "kernel", "launches"), x))
