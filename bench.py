@@ -658,16 +658,16 @@ def plan_cpu_baseline(route, wb, budget_s, status, groups):
     on a bounded sample of the same chunks; and the GPU's agreement with it on that sample."""
     import numpy as np
     import plan_oracle as PO
-    hw, threads, share = cpu_threads()
+    hw, full, threads = cpu_threads()
     po = PO.PlanOracle(route)
     B = wb["x0"].shape[0]
-    n = min(B, max(256, 8 * threads))                    # >= 8 chunks per thread
+    n = min(B, max(256, 8 * full))                       # >= 8 chunks per thread of the full-host run
     idx = np.linspace(0, B - 1, n).astype(int)           # spread over the horizons
     p = PO.default_params(N=int(wb["N"].max()))
     args = (wb["x0"][idx], wb["s_target"][idx], wb["is_final"][idx])
     ref = po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads)
     done, dt = _timed_rate(lambda: po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads), n, budget_s)
-    sdone, sdt = _timed_rate(lambda: po.solve_batch(p, *args, N=wb["N"][idx], num_threads=share), n, budget_s / 2)
+    sdone, sdt = _timed_rate(lambda: po.solve_batch(p, *args, N=wb["N"][idx], num_threads=full), n, budget_s / 3)
     # GPU vs oracle on the sample: X of chunks both call converged (status 0 / 4)
     dmax, agree, both = 0.0, 0, 0
     for j, i in enumerate(idx):
@@ -680,12 +680,15 @@ def plan_cpu_baseline(route, wb, budget_s, status, groups):
             both += 1
             dmax = max(dmax, float(np.abs(xg - ref["X"][j][:nn + 1]).max()))
     base = {"value": done / dt, "unit": "chunks/s", "cores": threads, "kind": "port", "host": hw,
-            "scope": "all physical host cores (lscpu)",
+            "scope": "this process's CPU share of the GPU box (cgroup quota)",
             "sample": f"{n} chunks spread over the batch (all horizons), solved repeatedly for {dt:.1f} s by the "
                       f"planner oracle (oracle/plan_oracle.c, the same SQP and QP algorithm) with OpenMP, "
                       f"{threads} threads",
-            "share": {"value": sdone / sdt, "unit": "chunks/s", "cores": share,
-                      "scope": "this GPU's share of the host (OMP_NUM_THREADS)"}}
+            "full_host": {"value": sdone / sdt, "unit": "chunks/s", "threads": full,
+                          "scope": "one thread per physical core of the host (lscpu), throttled to the quota"},
+            "whole_box_estimate": {"value": done / dt / threads * (hw["physical_cores_lscpu"] or full),
+                                   "cores": hw["physical_cores_lscpu"] or full,
+                                   "basis": "share rate per thread x physical cores (an estimate)"}}
     par = {"chunks": n, "status_agreement": agree / n, "both_converged": both, "max_abs_dX_both_converged": dmax}
     return base, par
 
@@ -717,28 +720,35 @@ def plan_cpu_reference(route, wb):
 def cpu_threads():
     """Thread counts of the CPU legs: 'full' = every physical core of the host (lscpu), bounded by the CPUs this
     process may run on, whatever OMP_NUM_THREADS the environment passes down (all physical host
-    cores of the GPU box); 'share' = this GPU's share of the host (OMP_NUM_THREADS, 16 on the GPU box), reported
-    beside it."""
+    cores of the GPU box); 'share' = this GPU's share of the host: the cgroup CPU quota (cpu.max), else
+    OMP_NUM_THREADS, else the affinity mask."""
     hw = host_cores()
     aff = hw["affinity_cpus"]
     full = min(hw["physical_cores_lscpu"] or aff, aff)
-    share = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff, aff)
-    return hw, full, share
+    q = hw.get("cgroup_cpu_quota")
+    share = int(q) if q else (int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff)
+    return hw, full, min(max(1, share), aff)
 
 
 def _timed_rate(fn, n, budget_s):
     fn()                                              # warm
-    done, t0 = 0, time.perf_counter()
+    done, t0, c0 = 0, time.perf_counter(), time.process_time()
     while time.perf_counter() - t0 < budget_s:
         fn()
         done += n
-    return done, time.perf_counter() - t0
+    dt = time.perf_counter() - t0
+    _timed_rate.cpu_per_wall = (time.process_time() - c0) / dt
+    return done, dt
 
 
 def cpu_baseline(wb, N, mo, budget_s):
-    """The oracle's C restatement (same QP, same PDIP), OpenMP over every physical core of the host, on the
-    whole per-GPU batch of the same egos, solved repeatedly for the budget; the same with this GPU's CPU share
-    as a secondary field.  kind = 'port' (the reference itself never travels to the GPU box)."""
+    """The oracle's C restatement (same QP, same PDIP), OpenMP, on the whole per-GPU batch of the same egos,
+    solved repeatedly for the budget, at three thread counts: this process's CPU share (the cgroup quota:
+    `value`, the best rate the box lets it measure), one thread (the per-core rate), and every physical core
+    of the host (on a quota-limited box those threads share the quota, so that run is
+    throttled and says so by its CPU-time / wall ratio).  The whole-host rate is then estimated as the per-core
+    rate of the share run x the physical cores (the solves are independent and compute-bound), and labelled an
+    estimate.  kind = 'port' (the reference itself never travels to the GPU box)."""
     import oracle as O
     import workloads as W
     ld = W.loader(wb["traj"])
@@ -747,14 +757,23 @@ def cpu_baseline(wb, N, mo, budget_s):
     hw, full, share = cpu_threads()
     n = wb["x0"].shape[0]
     out = {}
-    for tag, threads, budget in (("full", full, budget_s), ("share", share, budget_s / 2)):
+    for tag, threads, budget in (("share", share, budget_s), ("one", 1, budget_s / 4), ("full", full, budget_s / 3)):
         done, dt = _timed_rate(lambda: orc.solve_batch(p, wb["x0"], wb["obs"], wb["n_obs"], num_threads=threads),
                                n, budget)
-        out[tag] = {"value": done / dt, "unit": "solves/s", "cores": threads, "seconds": dt,
+        out[tag] = {"value": done / dt, "unit": "solves/s", "threads": threads, "seconds": dt,
+                    "cpu_time_per_wall": _timed_rate.cpu_per_wall,
                     "sample": f"the whole per-GPU batch ({n} egos), solved {done // n} times in {dt:.1f} s by the "
                               f"oracle's C PDIP (oracle/mpc_oracle.c) with OpenMP, {threads} threads"}
-    return dict(out["full"], kind="port", host=hw, scope="all physical host cores (lscpu)",
-                share=dict(out["share"], scope="this GPU's share of the host (OMP_NUM_THREADS)"))
+    phys = hw["physical_cores_lscpu"] or full
+    est = out["share"]["value"] / share * phys
+    return dict(out["share"], cores=share, kind="port", host=hw,
+                scope="this process's CPU share of the GPU box (cgroup quota)",
+                per_core=out["one"],
+                full_host=dict(out["full"], scope="one thread per physical core of the host (lscpu)",
+                               note="threads beyond the cgroup quota share it: CPU time / wall stays at the quota"),
+                whole_box_estimate={"value": est, "unit": "solves/s", "cores": phys,
+                                    "basis": f"share rate / {share} threads x {phys} physical cores (independent, "
+                                             "compute-bound solves; an estimate, not a measurement)"})
 
 
 def cpu_backend(wb, N, mo, budget_s):
@@ -767,7 +786,7 @@ def cpu_backend(wb, N, mo, budget_s):
     hw, full, share = cpu_threads()
     n = wb["x0"].shape[0]
     out = {}
-    for tag, threads in (("full", full), ("share", share)):
+    for tag, threads in (("share", share), ("full", full)):
         os.environ["MPC_CPU_THREADS"] = str(threads)
         slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo), device=-1)
         done, dt = _timed_rate(lambda: slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"]), n, budget_s / 2)
@@ -775,13 +794,15 @@ def cpu_backend(wb, N, mo, budget_s):
         out[tag] = {"value": done / dt, "unit": "solves/s", "cores": threads,
                     "sample": f"the whole per-GPU batch ({n} egos), solved {done // n} times in {dt:.1f} s by "
                               f"libmpcqp's host backend (device = -1), {threads} threads"}
-    return dict(out["full"], scope="all physical host cores (lscpu)",
-                share=dict(out["share"], scope="this GPU's share of the host (OMP_NUM_THREADS)"))
+    return dict(out["share"], scope="this process's CPU share of the GPU box (cgroup quota)",
+                full_host=dict(out["full"], scope="one thread per physical core of the host (lscpu), throttled to "
+                                                  "the quota"))
 
 
 def host_cores():
     """Host CPUs as the GPU box shows them: physical cores (lscpu, unique core/socket pairs) of the whole
-    machine, and the CPUs this process may run on (its affinity mask: the box's share)."""
+    machine, the CPUs this process may run on (its affinity mask), and the CPU time it may use per second
+    (the cgroup quota, cpu.max: 16 CPUs per GPU on the pool's boxes, whatever the affinity mask says)."""
     import subprocess
     phys = None
     try:
@@ -793,7 +814,15 @@ def host_cores():
         aff = len(os.sched_getaffinity(0))
     except Exception:
         aff = os.cpu_count() or 1
-    return {"physical_cores_lscpu": phys, "affinity_cpus": aff, "logical_cpus": os.cpu_count()}
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except Exception:
+        pass
+    return {"physical_cores_lscpu": phys, "affinity_cpus": aff, "logical_cpus": os.cpu_count(),
+            "cgroup_cpu_quota": quota}
 
 
 def cpu_reference(wb, N, budget_s):
