@@ -180,7 +180,7 @@ def main():
     rflops = riccati_flops(N, kmean) * B
     nbytes = algorithmic_bytes(N, mo) * B
     # PMC counters cannot be read inside this process (rocprofv3 collects them in their own runs,
-    # tools/gpu_bench_prof.sh); `traffic` is the per-step HBM bytes of the last such run of this config,
+    # tools/gpu/bench_profiles.sh); `traffic` is the per-step HBM bytes of the last such run of this config,
     # reported with the run it came from
     traffic, traffic_source = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_hbm_bytes.json")
@@ -262,9 +262,10 @@ def main():
         if plan is not None:
             out["plan"] = plan
         if not args.no_cpu and gpu:
-            out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
             out["cpu_backend"] = cpu_backend(wb, N, mo, min(args.cpu_seconds, 5.0))
             out["cpu_reference"] = cpu_reference(wb, N, args.cpu_seconds)
+            # last: its final run puts one thread on every physical core, beyond the process's CPU quota
+            out["cpu_baseline"] = cpu_baseline(wb, N, mo, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     comm.close()
 
@@ -601,7 +602,7 @@ def plan_leg(B, steps, route_name, comm, dev, cpu_s, with_cpu):
                "roofline": dict(executed_work("plan"), bound="fp64-valu", peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
                                 note="the chunk kernel is latency-bound (one wave per SIMD, sequential Riccati "
                                      "recursions, DESIGN.md 5c); executed FP64 from its PMC pass over N = 16, "
-                                     "16384 chunks (tools/gpu_plan_pmc.sh)"),
+                                     "16384 chunks (tools/gpu/plan_pmc_f64.sh)"),
                "note": "HIP events on the timing stream, which joins the side streams that run one launch per "
                        "residency class of horizons; inputs resident in HBM"}
         if with_cpu:
@@ -661,13 +662,12 @@ def plan_cpu_baseline(route, wb, budget_s, status, groups):
     hw, full, threads = cpu_threads()
     po = PO.PlanOracle(route)
     B = wb["x0"].shape[0]
-    n = min(B, max(256, 8 * full))                       # >= 8 chunks per thread of the full-host run
+    n = min(B, max(256, 16 * threads))                   # >= 16 chunks per thread
     idx = np.linspace(0, B - 1, n).astype(int)           # spread over the horizons
     p = PO.default_params(N=int(wb["N"].max()))
     args = (wb["x0"][idx], wb["s_target"][idx], wb["is_final"][idx])
     ref = po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads)
     done, dt = _timed_rate(lambda: po.solve_batch(p, *args, N=wb["N"][idx], num_threads=threads), n, budget_s)
-    sdone, sdt = _timed_rate(lambda: po.solve_batch(p, *args, N=wb["N"][idx], num_threads=full), n, budget_s / 3)
     # GPU vs oracle on the sample: X of chunks both call converged (status 0 / 4)
     dmax, agree, both = 0.0, 0, 0
     for j, i in enumerate(idx):
@@ -684,8 +684,6 @@ def plan_cpu_baseline(route, wb, budget_s, status, groups):
             "sample": f"{n} chunks spread over the batch (all horizons), solved repeatedly for {dt:.1f} s by the "
                       f"planner oracle (oracle/plan_oracle.c, the same SQP and QP algorithm) with OpenMP, "
                       f"{threads} threads",
-            "full_host": {"value": sdone / sdt, "unit": "chunks/s", "threads": full,
-                          "scope": "one thread per physical core of the host (lscpu), throttled to the quota"},
             "whole_box_estimate": {"value": done / dt / threads * (hw["physical_cores_lscpu"] or full),
                                    "cores": hw["physical_cores_lscpu"] or full,
                                    "basis": "share rate per thread x physical cores (an estimate)"}}
@@ -778,25 +776,20 @@ def cpu_baseline(wb, N, mo, budget_s):
 
 def cpu_backend(wb, N, mo, budget_s):
     """The product's own host backend (libmpcqp, mpc_create device = -1: csrc/cpu_backend.h) on the whole per-GPU
-    batch, every physical core of the host and this GPU's share: what a user without a GPU gets (config 1's CPU
-    path)."""
+    batch with this process's CPU share: what a user without a GPU gets (config 1's CPU path)."""
     import mpcqp
     import workloads as W
     ld = W.loader(wb["traj"])
     hw, full, share = cpu_threads()
     n = wb["x0"].shape[0]
-    out = {}
-    for tag, threads in (("share", share), ("full", full)):
-        os.environ["MPC_CPU_THREADS"] = str(threads)
-        slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo), device=-1)
-        done, dt = _timed_rate(lambda: slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"]), n, budget_s / 2)
-        slv.close()
-        out[tag] = {"value": done / dt, "unit": "solves/s", "cores": threads,
-                    "sample": f"the whole per-GPU batch ({n} egos), solved {done // n} times in {dt:.1f} s by "
-                              f"libmpcqp's host backend (device = -1), {threads} threads"}
-    return dict(out["share"], scope="this process's CPU share of the GPU box (cgroup quota)",
-                full_host=dict(out["full"], scope="one thread per physical core of the host (lscpu), throttled to "
-                                                  "the quota"))
+    os.environ["MPC_CPU_THREADS"] = str(share)
+    slv = mpcqp.Solver(ld.X_ref, ld.U_ref, mpcqp.default_params(N=N, max_obs=mo), device=-1)
+    done, dt = _timed_rate(lambda: slv.solve_batch(wb["x0"], wb["obs"], wb["n_obs"]), n, budget_s)
+    slv.close()
+    return {"value": done / dt, "unit": "solves/s", "cores": share,
+            "scope": "this process's CPU share of the GPU box (cgroup quota)",
+            "sample": f"the whole per-GPU batch ({n} egos), solved {done // n} times in {dt:.1f} s by libmpcqp's host "
+                      f"backend (device = -1), {share} threads"}
 
 
 def host_cores():

@@ -688,7 +688,10 @@ static int polish_from(const qpdat* Q, ipm_state* S, int* infeasible, int given,
         }
         riccati_factor(Q, &F);
         double X[MAXN + 1][5];
-        for (int r = 0; r <= POLISH_REFINE; ++r) {
+        /* the crossover from the all-inactive classification (given = 1) solves the unconstrained LQR: one solve
+         * is its exact optimum, nothing to refine (the kernel's MODE_XO runs one solve too) */
+        const int nref = given == 1 ? 1 : POLISH_REFINE;
+        for (int r = 0; r <= nref; ++r) {
             rollout_lin(Q, T.du, X);
             /* exact KKT residual of the equality QP; LQR right-hand side */
             double qh[MAXN + 1][5], gh[MAXN][2], r2[MAXN + 1][NROW], r2b[MAXN][NBOX];
@@ -720,7 +723,7 @@ static int polish_from(const qpdat* Q, ipm_state* S, int* infeasible, int given,
                     gh[t][box_comp[j]] += sg * r2b[t][j] / POLISH_DELTA;
                 }
             }
-            if (r == POLISH_REFINE) break;
+            if (r == nref) break;
             riccati_solve(Q, &F, qh, gh, &D);
             for (int i = 0; i < 2 * N; ++i) T.du[i] += D.du[i];
             for (int k = 1; k <= N; ++k)

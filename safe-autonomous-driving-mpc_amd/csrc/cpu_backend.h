@@ -586,7 +586,10 @@ private:
                     if (clb_[t][j]) F_.Rt[t][kBoxComp[j]] += 1.0 / kDelta;
             }
             riccati_factor();
-            for (int r = 0; r <= kRefine; ++r) {
+            // from the all-inactive classification (the crossover) the first solve is the unconstrained LQR's exact
+            // optimum: one solve, nothing to refine (oracle polish_from, kernel MODE_XO)
+            const int nref = from == 1 ? 1 : kRefine;
+            for (int r = 0; r <= nref; ++r) {
                 rollout(W.du, Xs);
                 double qh[kMaxN + 1][5], gh[kMaxN][2], r2[kMaxN + 1][kRows], r2b[kMaxN][kBox];
                 for (int k = 1; k <= N; ++k) {
@@ -616,7 +619,7 @@ private:
                         gh[t][kBoxComp[j]] += sg * r2b[t][j] / kDelta;
                     }
                 }
-                if (r == kRefine) break;
+                if (r == nref) break;
                 riccati_solve(qh, gh, D_);
                 for (int i = 0; i < 2 * N; ++i) W.du[i] += D_.du[i];
                 for (int k = 1; k <= N; ++k)

@@ -1764,8 +1764,12 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 double xp[4] = {x4[0], x4[1], x4[2], x4[3]};
                 pu0 = du0;
                 pu1 = du1;
+                // the crossover from the all-inactive classification solves the unconstrained LQR: the first solve
+                // is its exact optimum (no active-row penalties to refine), so it runs one solve, not
+                // POLISH_REFINE (oracle polish_from, host backend active_set)
+                const int nref = (phase == 0 && !(MODE == MODE_FULL && sqp > 0)) ? 1 : POLISH_REFINE;
 #pragma unroll 1
-                for (int r = 0; r < POLISH_REFINE; ++r) {
+                for (int r = 0; r < nref; ++r) {
                     // exact KKT residual of the equality QP -> LQR right-hand side
                     double r2[NR], r2b[NBOX];
 #pragma unroll

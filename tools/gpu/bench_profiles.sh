@@ -15,4 +15,4 @@ cd $R && python tools/pmc_summary.py C2 ${ROUND:-} ${COMMIT:-}
 find gpurun_out/prof_stats -name "*kernel_stats*"
 : > gpurun_out/phase.log
 timeout -k 10 200 python tools/phase_probe.py C2 4096 >> gpurun_out/phase.log 2>&1 && PROBE_WORST=1 timeout -k 10 200 python tools/phase_probe.py C2 1 >> gpurun_out/phase.log 2>&1 || { echo "phase probe failed"; tail gpurun_out/phase.log; exit 1; }
-bash tools/gpu_configs.sh
+bash tools/gpu/configs.sh

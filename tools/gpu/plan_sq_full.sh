@@ -1,5 +1,5 @@
 # Round 5: SQ wait classes of a full planner launch (1024 chunks at N = 16, four waves per CU) against the
-# slowest chunk alone (tools/gpu_r05_plan_sq.sh): where the 2.4x per-iteration cost of a full launch goes.
+# slowest chunk alone (tools/gpu/plan_sq_worst.sh): where the 2.4x per-iteration cost of a full launch goes.
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp

@@ -9,4 +9,4 @@ B="python3 $R/bench.py --no-cpu --inflight 0 --nlp-steps 0 --closed-loop 0 --pla
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_stats -o run --output-format csv -- $B --steps 20 --warmup 3 > $R/gpurun_out/prof_stats.log 2>&1 || { echo "stats failed"; tail $R/gpurun_out/prof_stats.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- $B --steps 3 --warmup 1 > $R/gpurun_out/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail $R/gpurun_out/pmc_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- $B --steps 3 --warmup 1 > $R/gpurun_out/pmc_write.log 2>&1 || { echo "pmc write failed"; tail $R/gpurun_out/pmc_write.log; exit 1; }
-cd $R && bash tools/gpu_configs.sh
+cd $R && bash tools/gpu/configs.sh

@@ -12,7 +12,7 @@ import torch
 import mpcplan
 import workloads as W
 
-if os.environ.get("PLAN_LIB"):      # A/B of library variants (tools/gpu_plan_lib_ab.sh)
+if os.environ.get("PLAN_LIB"):      # A/B of library variants (gpu_plan_lib_ab.sh (removed in round 6))
     mpcplan.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", os.environ["PLAN_LIB"])
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 20

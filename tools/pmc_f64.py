@@ -1,4 +1,4 @@
-"""Summarise the executed-work PMC pass (tools/gpu_f64_pmc.sh) per solver kernel.
+"""Summarise the executed-work PMC pass (tools/gpu/pmc_f64.sh) per solver kernel.
 
 Per launch of each kernel (mode XO / IPM / FULL / ONE, template <OBS, G, MODE, NT>):
 - FP64 VALU instructions by class (SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64, summed over all waves);

@@ -1,4 +1,4 @@
-"""Summary of tools/gpu_r05_pmc_reads.sh: per-dispatch counter means of the C2 solver kernels (crossover
+"""Summary of tools/gpu/pmc_reads.sh: per-dispatch counter means of the C2 solver kernels (crossover
 MODE_XO, interior point MODE_IPM) for each pass, and a linear fit over B of FETCH_SIZE per kernel (per-launch
 intercept vs per-instance slope).  Writes profiles/r05_pmc_reads.csv and prints a table, then the attribution: each kernel's code-object
 size (C2: MODE_IPM / MODE_XO instantiation at N = 20 without obstacles) times the 8 XCDs, whose L2s each
