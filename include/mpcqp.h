@@ -30,8 +30,9 @@ extern "C" {
 #endif
 
 /* 2: status[] / hist_status[] may carry the MPC_SQP_UNCONVERGED flag (16) OR-ed onto the code; mask with
- *    MPC_STATUS_MASK before comparing with MPC_OK .. MPC_NUMERICAL (version 1 returned 0-3 only). */
-#define MPCQP_VERSION 2
+ *    MPC_STATUS_MASK before comparing with MPC_OK .. MPC_NUMERICAL (version 1 returned 0-3 only).
+ * 3: the ego-shard communicator (mpc_comm_*, mpc_gather*, MPC_E_COMM); nothing else changed. */
+#define MPCQP_VERSION 3
 #define MPC_MAX_N 63          /* horizon limit (one lane per stage k=0..N in the kernel)   */
 #define MPC_MAX_OBS 64        /* obstacle slab limit per instance                            */
 
@@ -121,13 +122,13 @@ int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, cons
  * with 16-byte stores when both are 16-byte aligned, else with 8-byte ones.  No host synchronisation and,
  * once warmed up, no allocation (graph-capturable): the
  * two-phase work list is allocated by mpc_create for up to 2^20 instances (a larger B runs the
- * single-kernel path, same results).  With MPC_STAGE_CACHE=1 in the environment (off by default) the
- * two-phase launch also keeps the deferred instances' linearisation point and rollout (7N+5 doubles
- * each) in a cache that grows on the first eager call with a larger B (hipMalloc, which waits for the
- * device); a captured call never uses it (a later eager call may grow it, which would leave the graph
- * with a freed pointer), same results.  The work list belongs to the context: consecutive eager calls on
- * one context are ordered
- * on the device even when they use different streams (a call on a new stream waits for the previous
+ * single-kernel path, same results).  The two-phase launch keeps, per deferred instance, its linearisation
+ * point, nominal rollout and the crossover's solve (the interior point's start; 13N+5 doubles) in a stage
+ * cache that grows on the first eager call with a larger B (hipMalloc, which waits for the device; at most
+ * 1 GiB, MPC_STAGE_CACHE=0 switches it off); a captured call never uses it (a later eager call may grow it,
+ * which would leave the graph with a freed pointer) and recomputes the start bit for bit instead.  The work
+ * list belongs to the context: consecutive eager calls on one context are ordered on the device even when
+ * they use different streams (a call on a new stream waits for the previous
  * call's kernels), so their results never depend on the streams chosen.  A call made while `stream` is
  * being captured into a HIP graph records no such ordering (it would tie the graph to work outside
  * it): replays of that graph must not overlap eager calls, or replays of another graph, on the same

@@ -648,6 +648,9 @@ static int check_on(void) {
 static __thread unsigned char last_cls[MAXN + 1][NROW], last_clb[MAXN][NBOX];
 /* given = 1: start from the all-inactive classification (crossover) instead of classifying S;
  * given = 2: start from the previous QP's classification (last_cls / last_clb) */
+/* du of the last crossover's solve from the all-inactive classification (given = 1): the unconstrained optimum
+ * of QP(ubar), which the interior point's start then reuses instead of a second factorisation and solve */
+static __thread double xo_du[2 * MAXN];
 static int polish_from(const qpdat* Q, ipm_state* S, int* infeasible, int given, int rounds) {
     int N = Q->N;
     double rho = Q->rho;
@@ -735,6 +738,8 @@ static int polish_from(const qpdat* Q, ipm_state* S, int* infeasible, int given,
                     if (clb[t][j])
                         T.lb[t][j] += (r2b[t][j] - box_sign[j] * D.du[2 * t + box_comp[j]]) / POLISH_DELTA;
         }
+        /* the crossover's solve is the unconstrained optimum of QP(ubar): kept for the interior-point start */
+        if (given == 1 && round == 0) memcpy(xo_du, T.du, sizeof(double) * 2 * N);
         /* acceptance: KKT consistency of the polished point; otherwise fix the worst row and retry */
         double lmax = 1.0;
         for (int k = 1; k <= N; ++k)
@@ -854,7 +859,11 @@ static int pdip(const qpdat* Q, const mpc_params* p, ipm_state* S, int* iters, i
      * complementarity, sb >= 1).  With tol_mu 1e-10 (round 2: the start at du = 0 with s lam = 1000,
      * lam <= rho/2, and 1e-9), maximum iterations C2 22 -> 20, C3 24 -> 22, C4 27 -> 25, C5 29 -> 27, and
      * every feasible C5 instance polish-certified. */
-    {
+    if (p->polish >= 2 && !warm) {
+        /* the crossover above solved exactly this system (all rows inactive: the stage Hessians and the
+         * right-hand side -q, -r of the start); its solution is the start's, bit for bit */
+        memcpy(S->du, xo_du, sizeof(double) * 2 * N);
+    } else {
         static __thread ipm_fact F0;
         static __thread ipm_dir D0;
         double qh[MAXN + 1][5], gh[MAXN][2];

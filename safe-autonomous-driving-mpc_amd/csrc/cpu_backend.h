@@ -234,6 +234,7 @@ private:
     unsigned char cls_[kMaxN + 1][kRows], clb_[kMaxN][kBox];      // 0 inactive, 1 active, 2 violated
     unsigned char flip_[kMaxN + 1][kRows], flipb_[kMaxN][kBox];
     unsigned char last_cls_[kMaxN + 1][kRows], last_clb_[kMaxN][kBox];   // the SQP's warm crossover
+    double xo_du_[2 * kMaxN];   // du of the last cold crossover solve: the unconstrained optimum (interior-point start)
 
     // ---- QP(ubar): Gauss-Newton model of cost/constraints around the nominal rollout
     void build(const double x0[5], const double* obs, int nobs, const double* ub) {
@@ -629,6 +630,8 @@ private:
                     for (int j = 0; j < kBox; ++j)
                         if (clb_[t][j]) W.lb[t][j] += (r2b[t][j] - kBoxSign[j] * D_.du[2 * t + kBoxComp[j]]) / kDelta;
             }
+            // the crossover's solve is the unconstrained optimum of QP(ubar): kept for the interior-point start
+            if (from == 1 && round == 0) std::memcpy(xo_du_, W.du, sizeof(double) * 2 * N);
             // KKT consistency of the solved point
             double lmax = 1.0;
             for (int k = 1; k <= N; ++k)
@@ -711,7 +714,10 @@ private:
         // slack max(r, 0) + shift, elastic slack max(-r, 0) + shift for the row value r there, the multiplier
         // pair on the pair's central path with lambda + nu = rho; box rows at the mean row complementarity
         double X[kMaxN + 1][5];
-        {
+        if (p_.polish >= 2 && !warm) {
+            // the crossover solved exactly this system (all rows inactive): its solution is the start's
+            std::memcpy(S_.du, xo_du_, sizeof(double) * 2 * N);
+        } else {
             double qh[kMaxN + 1][5], gh[kMaxN][2];
             for (int k = 1; k <= N; ++k) {
                 std::memcpy(F_.Qt[k], Q.Q[k], sizeof(F_.Qt[k]));

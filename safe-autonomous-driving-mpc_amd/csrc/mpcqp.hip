@@ -202,8 +202,11 @@ __host__ __device__ constexpr bool acl_on(int GL, int NT) { return NT > 0 || GL 
 #define DQ_ZC 8
 #define DQ_ZA 10
 
-// stage cache record of the split launch, per work-list slot: ub [N][2] then Xr [N+1][5]
-__host__ __device__ constexpr int stage_cache_doubles(int N) { return 2 * N + 5 * (N + 1); }
+// stage cache record of the split launch, per work-list slot: ub [N][2], Xr [N+1][5], then the crossover's solve
+// (the unconstrained optimum of QP(ubar), the interior point's start) by lane: du of control k-1 and x4 of
+// stage k, [N][6]
+__host__ __device__ constexpr int stage_cache_doubles(int N) { return 2 * N + 5 * (N + 1) + 6 * N; }
+__host__ __device__ constexpr int stage_cache_xo(int N) { return 2 * N + 5 * (N + 1); }
 
 __host__ __device__ inline int lds_doubles(int N, bool acl, bool lite = false) {
     int NP = N + 1;
@@ -1305,7 +1308,13 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             // multiplier pair the pair's central point with lambda + nu = rho; box rows the mean row
             // complementarity.  (Round 2 started at du = 0 with s lam = 1000, lam <= rho / 2 and stopped at
             // mu <= 1e-9: C2 22 -> 20 iterations at most, C5 29 -> 27)
-            if (live) {
+            // The crossover (phase 0 from the all-inactive classification) solved exactly this system: the same
+            // factorisation inputs and right-hand side, in the same solve form, so its solution is the start's
+            // bit for bit.  MODE_FULL / MODE_ONE still hold it in dX / dud; MODE_IPM reads it from the stage
+            // cache; otherwise (no crossover ran, a warm SQP crossover, or no cache) it is recomputed here, in
+            // the crossover's solve form (the K-row form wherever the split launch exists, G >= 2).
+            const bool xo_start = (MODE == MODE_IPM) ? cached : (phase_lo == 0 && !(MODE == MODE_FULL && sqp > 0));
+            if (live && !xo_start) {
                 double Qs[10], qs[4];
                 stage_cost(LITE ? cstr : S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
 #pragma unroll
@@ -1321,13 +1330,24 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 S.gh[2 * (k - 1)] = -(R0 * S.ub[2 * (k - 1)]);
                 S.gh[2 * (k - 1) + 1] = -(R1 * S.ub[2 * (k - 1) + 1]);
             }
-            wave_sync();
-            riccati_factor<NT>(S, N, dt, gl);
-            riccati_solve<NTR, ACL>(S, N, dt, gl);
+            if (!xo_start) {
+                wave_sync();
+                riccati_factor<NT>(S, N, dt, gl);
+                if constexpr (ACL && GL == 64) riccati_solve<NTR, ACL>(S, N, dt, gl);
+                else riccati_solve<NTR, false>(S, N, dt, gl);
+            }
+            if (MODE == MODE_IPM && cached) {
+                const double* xo = stc_in + stage_cache_xo(N) + 6 * (live ? k - 1 : 0);
+                du0 = live ? xo[0] : 0.0;
+                du1 = live ? xo[1] : 0.0;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) x4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
-            du0 = live ? S.dud[2 * (k - 1)] : 0.0;
-            du1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
+                for (int a = 0; a < 4; ++a) x4[a] = live ? xo[2 + a] : 0.0;
+            } else {
+#pragma unroll
+                for (int a = 0; a < 4; ++a) x4[a] = live ? S.dX[5 * k + st4(a)] : 0.0;
+                du0 = live ? S.dud[2 * (k - 1)] : 0.0;
+                du1 = live ? S.dud[2 * (k - 1) + 1] : 0.0;
+            }
             {
                 // primal point: the unconstrained optimum, or du = 0 (the warm start ubar, which already brakes
                 // for obstacles ahead) when the soft rows are less violated there (sum of max(-r, 0))
@@ -1982,6 +2002,15 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 o[2 * gl + 1] = S.ub[2 * gl + 1];
             }
             for (int i = gl; i < 5 * NP; i += GL) o[2 * N + i] = S.Xr[i];
+            // the crossover's solve (the interior point's start): still in dud / dX (the epilogue's rollout
+            // writes Xr and kap only)
+            if (gl < N) {
+                double* xo = o + stage_cache_xo(N) + 6 * gl;
+                xo[0] = S.dud[2 * gl];
+                xo[1] = S.dud[2 * gl + 1];
+#pragma unroll
+                for (int a = 0; a < 4; ++a) xo[2 + a] = S.dX[5 * (gl + 1) + st4(a)];
+            }
         }
     } else if (bvalid) {
         // one 16-B store per lane (full cache lines, not two half-filled strided stores) when the caller's
@@ -2396,7 +2425,7 @@ extern "C" int mpc_create(const double* X, int T, const double* U, int Tu, const
         const char* e = std::getenv("MPC_TWO_PHASE");
         c->two_phase = !(e && e[0] == '0');
         const char* e2 = std::getenv("MPC_STAGE_CACHE");
-        c->use_stc = e2 && e2[0] == '1';
+        c->use_stc = !(e2 && e2[0] == '0');     // on by default since round 6 (it carries the interior point's start)
         const char* e3 = std::getenv("MPC_WL_MEMSET");
         c->wl_memset = e3 && e3[0] == '1';
         const char* e4 = std::getenv("MPC_IPM_GL64");
@@ -2492,6 +2521,7 @@ extern "C" void mpc_destroy(mpc_ctx* c) {
 }
 
 // launch of the solver kernel for an already validated parameter set
+#define MPC_STAGE_CACHE_CAP ((size_t)1 << 27)
 static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, const double* obs, const int* n_obs,
                         const double* ubar, double* u0, double* U, double* Xpred, int* status, int* iters,
                         hipStream_t st) {
@@ -2530,7 +2560,9 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
         if (!capturing && c->wl_pending && c->wl_stream != st)
             HIPCHK(hipStreamWaitEvent(st, c->wl_done, 0), MPC_E_DEVICE);
         const size_t need = (size_t)B * stage_cache_doubles(kp.N);
-        if (c->use_stc && need > c->cap_stc && !capturing) {
+        // the cache is sized for B records (only the deferred instances write one); above MPC_STAGE_CACHE_CAP
+        // doubles (1 GiB) the call runs without it (the same results: the start is recomputed bit for bit)
+        if (c->use_stc && need > c->cap_stc && need <= MPC_STAGE_CACHE_CAP && !capturing) {
             // hipFree waits for the device, so no launch still reads the old buffer
             hipFree(c->stc);
             c->stc = nullptr;
