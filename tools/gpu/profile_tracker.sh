@@ -20,6 +20,6 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run
 cd $R
 STATS=$(find gpurun_out/prof_stats -name '*kernel_stats.csv' | head -1)
 cp $STATS $OUT/${ROUND}_kernel_stats.csv
-python3 tools/pmc_f64.py $CFG $STATS > $OUT/pmc_f64.json && cp gpurun_out/pmc_f64_$CFG.csv $OUT/${ROUND}_pmc_f64_$CFG.csv
+python3 tools/pmc_f64.py $CFG $OUT/${ROUND}_kernel_stats.csv > $OUT/pmc_f64.json && cp gpurun_out/pmc_f64_$CFG.csv $OUT/${ROUND}_pmc_f64_$CFG.csv
 python3 tools/pmc_summary.py $CFG $ROUND ${COMMIT:-unknown} > $OUT/pmc_hbm.txt && cp profiles/pmc_hbm_bytes.json $OUT/pmc_hbm_bytes.json
 ls $OUT; head -3 $OUT/${ROUND}_kernel_stats.csv; cat $OUT/pmc_hbm.txt | tail -3
