@@ -486,7 +486,11 @@ __device__ __forceinline__ void lds_fence() {
     __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0), vmcnt/expcnt untouched
     __builtin_amdgcn_sched_barrier(0);
 }
+#ifdef MPC_NO_SCHED_FENCE
+__device__ __forceinline__ void sched_fence() {}
+#else
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+#endif
 
 // ------------------------------------------------------------------------------------------
 // distributed recursions.  The Riccati factorisation and solves run on lanes i = 0..4 of each
@@ -757,17 +761,21 @@ __device__ __forceinline__ void kk_stage(const Lds& S, int t, double dt) {
     S.KR[KRS * t + 11] = k1;
 }
 // closed-loop rows 3, 4 of stage t for the forward solve: e_{3+r}' + dt K_t(r,:) and dt kk_r
+// Every LDS read of a stage-parallel phase is issued before its first LDS write: the compiler cannot tell the
+// arrays of the layout apart, so a read after a write would wait for it (one LDS round trip per element)
 __device__ __forceinline__ void ac_rows(const Lds& S, int t, double dt) {
     const double* kr = S.KR + KRS * t;
     double* ac = S.AC + 30 * t + 18;
+    double k[2][6];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int m = 0; m < 6; m += 2) ld2(kr + 6 * r + m, k[r][m], k[r][m + 1]);
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-        double k[6];
 #pragma unroll
-        for (int m = 0; m < 6; m += 2) ld2(kr + 6 * r + m, k[m], k[m + 1]);
-#pragma unroll
-        for (int m = 0; m < 5; ++m) ac[6 * r + m] = (m == 3 + r) ? fma(dt, k[m], 1.0) : dt * k[m];
-        ac[6 * r + 5] = dt * k[5];
+        for (int m = 0; m < 5; ++m) ac[6 * r + m] = (m == 3 + r) ? fma(dt, k[r][m], 1.0) : dt * k[r][m];
+        ac[6 * r + 5] = dt * k[r][5];
     }
 }
 // u_t = kk_t + K_t x_t after the closed-loop forward solve (stage-parallel; the accumulation order of
@@ -775,19 +783,21 @@ __device__ __forceinline__ void ac_rows(const Lds& S, int t, double dt) {
 __device__ __forceinline__ void u_stage(const Lds& S, int t) {
     const double* kr = S.KR + KRS * t;
     const double* x = S.dX + 5 * t;
-    double xv[5];
+    double xv[5], k[2][6];
 #pragma unroll
     for (int m = 0; m < 5; ++m) xv[m] = x[m];
 #pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int m = 0; m < 6; m += 2) ld2(kr + 6 * r + m, k[r][m], k[r][m + 1]);
+    double u[2];
+#pragma unroll
     for (int r = 0; r < 2; ++r) {
-        double k[6];
+        u[r] = k[r][5];
 #pragma unroll
-        for (int m = 0; m < 6; m += 2) ld2(kr + 6 * r + m, k[m], k[m + 1]);
-        double u = k[5];
-#pragma unroll
-        for (int m = 0; m < 5; ++m) u = fma(xv[m], k[m], u);
-        S.dud[2 * t + r] = u;
+        for (int m = 0; m < 5; ++m) u[r] = fma(xv[m], k[r][m], u[r]);
     }
+    *reinterpret_cast<double2*>(S.dud + 2 * t) = make_double2(u[0], u[1]);
 }
 struct AclRec { double c[5], d; };
 __device__ __forceinline__ void load_acl(const Lds& S, const DLane& L, int t, AclRec& F) {
@@ -1393,10 +1403,12 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             PROF(1)
             // the row bounds are loop-invariant; keeping them opaque stops the compiler from hoisting
             // everything derived from them out of this loop (it would stay live in registers and spill)
+#ifndef MPC_NO_BK_OPAQUE
 #pragma unroll
             for (int j = 0; j < NR; ++j) asm volatile("" : "+v"(bk[j]));
 #pragma unroll
             for (int j = 0; j < NBOX; ++j) asm volatile("" : "+v"(bb[j]));
+#endif
             // -- stage-parallel residuals ------------------------------------------------------
             double rpmax = 0.0, rxmax = 0.0, comp = 0.0;
             double ya[4] = {0, 0, 0, 0};
@@ -1596,12 +1608,16 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         if (j < 2) g0 += bsign(j) * w; else g1 += bsign(j) * w;
                     }
                     if (live) {
+                        // the dual-residual terms are read before any write (see ac_rows)
+                        double ysv[4], zs0, zs1;
+                        ld2(S.ys + 4 * k, ysv[0], ysv[1]);
+                        ld2(S.ys + 4 * k + 2, ysv[2], ysv[3]);
+                        ld2(S.zs + 2 * (k - 1), zs0, zs1);
 #pragma unroll
-                        for (int a = 0; a < 4; ++a) S.QH[QHS * k + st4(a)] = q4[a] - S.ys[4 * k + a];
+                        for (int a = 0; a < 4; ++a) S.QH[QHS * k + st4(a)] = q4[a] - ysv[a];
                         S.QH[QHS * k + 3] = 0.0;
                         S.QH[QHS * k + 5] = 0.0;
-                        S.gh[2 * (k - 1)] = g0 - S.zs[2 * (k - 1)];
-                        S.gh[2 * (k - 1) + 1] = g1 - S.zs[2 * (k - 1) + 1];
+                        *reinterpret_cast<double2*>(S.gh + 2 * (k - 1)) = make_double2(g0 - zs0, g1 - zs1);
                     }
                 }
                 wave_sync();
@@ -1810,8 +1826,9 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                             const double v = (clb[j] == 1) ? bsign(j) * (tlb[j] + r2b[j] * (1.0 / POLISH_DELTA)) : 0.0;
                             if (j < 2) g0 += v; else g1 += v;
                         }
-                        double Qs[10], qs[4];
+                        double Qs[10], qs[4], ub0, ub1;
                         stage_cost(LITE ? cstr : S.cst + 6 * k, Pr.w_d, Pr.w_o, Pr.w_v, Qs, qs);
+                        ld2(S.ub + 2 * (k - 1), ub0, ub1);        // reads before the writes (see ac_rows)
 #pragma unroll
                         for (int a = 0; a < 4; ++a) {
                             double acc = qs[a];
@@ -1821,8 +1838,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                         }
                         S.QH[QHS * k + 3] = 0.0;
                         S.QH[QHS * k + 5] = 0.0;
-                        S.gh[2 * (k - 1)] = g0 - fma(R0, pu0, R0 * S.ub[2 * (k - 1)]);
-                        S.gh[2 * (k - 1) + 1] = g1 - fma(R1, pu1, R1 * S.ub[2 * (k - 1) + 1]);
+                        *reinterpret_cast<double2*>(S.gh + 2 * (k - 1)) =
+                            make_double2(g0 - fma(R0, pu0, R0 * ub0), g1 - fma(R1, pu1, R1 * ub1));
                     }
                     wave_sync();
                     // the crossover (phase 0) solves in K-row form wherever the two-phase launch exists
@@ -2593,6 +2610,14 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
                        MODEV == MODE_XO ? wnext : nullptr)
     // horizon-specialised kernels for the BASELINE horizons (N = 20: C2, C3; N = 30: C4; N = 40: C5), whose
     // unrolled recursions pay for their code size (C4 0.89 -> 0.66 ms, C5 5.67 -> 4.16 ms)
+#ifdef MPC_AB_NT20ONLY
+    // experiment builds only (tools/build_variant.sh): the N = 20 kernels alone, which compile ~4x faster
+#define MPC_LAUNCH_GL(MODEV)                                                                   \
+    do {                                                                                       \
+        if (!nt20) return fail(MPC_E_ARG, "MPC_AB_NT20ONLY build: N = 20 only");             \
+        if (with_obs) MPC_LAUNCH(32, true, MODEV, 20); else MPC_LAUNCH(32, false, MODEV, 20);  \
+    } while (0)
+#else
 #define MPC_LAUNCH_GL(MODEV)                                                                   \
     do {                                                                                       \
         if (nt20) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 20); else MPC_LAUNCH(32, false, MODEV, 20); } \
@@ -2602,12 +2627,14 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
         else if (GL == 32) { if (with_obs) MPC_LAUNCH(32, true, MODEV, 0); else MPC_LAUNCH(32, false, MODEV, 0); } \
         else { if (with_obs) MPC_LAUNCH(64, true, MODEV, 0); else MPC_LAUNCH(64, false, MODEV, 0); } \
     } while (0)
+#endif
     const bool with_obs = obs != nullptr && kp.max_obs > 0;
     if (split) {
         MPC_LAUNCH_GL(MODE_XO);
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
         // the launched MODE_XO zeroed wl[epoch ^ 1] and uses wl[epoch]: the next eager call takes the other
         if (wnext) c->wl_epoch ^= 1;
+#ifndef MPC_AB_NT20ONLY
         if (nt20 && c->ipm_gl64) {
             // one deferred instance per wavefront: B waves at most, the wave's LDS for one group
             const size_t lds_one = sizeof(double) * (size_t)lds_doubles(kp.N, true);
@@ -2619,7 +2646,9 @@ static int launch_solve(mpc_ctx* c, const KParams& kp, int B, const double* x0, 
                 hipLaunchKernelGGL((mpc_solve_kernel<64, false, MODE_IPM, 20>), dim3(B), dim3(WAVE), lds_one, st,
                                    c->tab, kp, B, x0, obs, nob, ubar, u0, U, Xpred, status, iters, wl, wcnt, stc,
                                    nullptr);
-        } else {
+        } else
+#endif
+        {
             MPC_LAUNCH_GL(MODE_IPM);
         }
         HIPCHK(hipGetLastError(), MPC_E_LAUNCH);
