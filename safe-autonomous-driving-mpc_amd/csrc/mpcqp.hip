@@ -587,17 +587,53 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
     const double c0 = dt * il00, c1 = dt * il11, c2 = -l10 * il11;
     // row i of M = P A (local)
     double m[5];
+#ifndef MPC_FAC_NOP
+    // (update stages: m[0], m[2..4] are formed inside the A'M block below, so that block needs no s_nop)
+    if (!upd) {
+#endif
     m[0] = fma(pr[2], a20, pr[0]);
     m[1] = pr[1];
     m[2] = fma(pr[1], a12, pr[2]);
     m[3] = fma(pr[2], a23, pr[3]);
     m[4] = fma(pr[0], dt, fma(pr[1], a14, fma(pr[2], a24, pr[4])));
+#ifndef MPC_FAC_NOP
+    }
+#endif
     // row i of A'M = M(i,:) + sum_l J'(l,i) M(l,:), and V3 = M(3,i), V4 = M(4,i) = P(i,{3,4}) +
     // sum_l J'(l,i) P(l,{3,4}), all in place.  Source lane l only changes in the broadcast of a lane l'
     // with J'(l',l) != 0; with J' nonzero at (0,4), (1,2), (1,4), (2,0), (2,3), (2,4) the order l = 0, 2, 1
     // reads every source lane before its own update (a zero coefficient leaves a value unchanged).
     // The same register is written and then broadcast 7 instructions later (the DPP hazard needs 2).
     double v3 = pr[3], v4 = pr[4];
+#ifndef MPC_FAC_NOP
+    if (upd) {
+        // The VALU-write -> DPP-read hazard (2 wait states) without an s_nop: the block first forms the rows of
+        // M = P A it broadcasts (the same fma()s as above, in the same order), so every register a DPP reads was
+        // written at least 2 instructions earlier inside the block (m[0] 5 before the first broadcast, m[4]
+        // 4 before its own), and whatever the compiler wrote before the block is 6 or more instructions back.
+        m[1] = pr[1];
+        asm("v_fma_f64 %0, %10, %13, %11\n\t"          // m0 = fma(p2, a20, p0)
+            "v_fma_f64 %2, %12, %14, %10\n\t"          // m2 = fma(p1, a12, p2)
+            "v_fma_f64 %3, %10, %15, %16\n\t"          // m3 = fma(p2, a23, p3)
+            "v_fma_f64 %4, %10, %17, %18\n\t"          // t = fma(p2, a24, p4)
+            "v_fma_f64 %4, %12, %19, %4\n\t"           // t = fma(p1, a14, t)
+            "v_fma_f64 %4, %11, %20, %4\n\t"           // m4 = fma(p0, dt, t)
+            DPPF("%0", "%0", "%7", 0) DPPF("%1", "%1", "%7", 0) DPPF("%2", "%2", "%7", 0) DPPF("%3", "%3", "%7", 0)
+            DPPF("%4", "%4", "%7", 0) DPPF("%5", "%5", "%7", 0) DPPF("%6", "%6", "%7", 0)
+            DPPF("%0", "%0", "%8", 2) DPPF("%1", "%1", "%8", 2) DPPF("%2", "%2", "%8", 2) DPPF("%3", "%3", "%8", 2)
+            DPPF("%4", "%4", "%8", 2) DPPF("%5", "%5", "%8", 2) DPPF("%6", "%6", "%8", 2)
+            DPPF("%0", "%0", "%9", 1) DPPF("%1", "%1", "%9", 1) DPPF("%2", "%2", "%9", 1) DPPF("%3", "%3", "%9", 1)
+            DPPF("%4", "%4", "%9", 1) DPPF("%5", "%5", "%9", 1) DPPF("%6", "%6", "%9", 1)
+            : "=&v"(m[0]), "+&v"(m[1]), "=&v"(m[2]), "=&v"(m[3]), "=&v"(m[4]), "+&v"(v3), "+&v"(v4)
+            : "v"(L.e0), "v"(F.e2), "v"(F.e1), "v"(pr[2]), "v"(pr[0]), "v"(pr[1]),
+              "v"(a20), "v"(a12), "v"(a23), "v"(pr[3]), "v"(a24), "v"(pr[4]), "v"(a14), "v"(dt));
+    } else {
+        asm("s_nop 1\n\t" DPPF("%0", "%0", "%2", 0) DPPF("%1", "%1", "%2", 0) "s_nop 1\n\t"
+            DPPF("%0", "%0", "%3", 2) DPPF("%1", "%1", "%3", 2) "s_nop 1\n\t"
+            DPPF("%0", "%0", "%4", 1) DPPF("%1", "%1", "%4", 1)
+            : "+v"(v3), "+v"(v4) : "v"(L.e0), "v"(F.e2), "v"(F.e1));
+    }
+#else
     if (upd) {
         asm("s_nop 1\n\t"
             DPPF("%0", "%0", "%7", 0) DPPF("%1", "%1", "%7", 0) DPPF("%2", "%2", "%7", 0) DPPF("%3", "%3", "%7", 0)
@@ -614,11 +650,36 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
             DPPF("%0", "%0", "%4", 1) DPPF("%1", "%1", "%4", 1)
             : "+v"(v3), "+v"(v4) : "v"(L.e0), "v"(F.e2), "v"(F.e1));
     }
+#endif
     double* am = m;
-    const double w0 = c0 * v3;
-    const double w1 = fma(c1, v4, c2 * w0);
-    const double K1 = -w1 * il11;
-    const double K0 = -(w0 + l10 * K1) * il00;
+    double w0, w1, K1, K0;
+#ifndef MPC_FAC_NOP
+    if (upd) {
+        // W, K and then P -= W'W: the block first forms w0, w1, K1, K0 (the same operations as below, in the
+        // same order, no contraction), so w1 is 4 instructions old at its first broadcast: no s_nop
+        double tt;
+        asm("v_mul_f64 %5, %9, %10\n\t"                // w0 = c0 * v3
+            "v_mul_f64 %7, %11, %5\n\t"                // t = c2 * w0
+            "v_fma_f64 %6, %12, %13, %7\n\t"           // w1 = fma(c1, v4, t)
+            "v_mul_f64 %8, -%6, %14\n\t"               // K1 = -w1 * il11
+            "v_mul_f64 %7, %15, %8\n\t"                // t = l10 * K1
+            "v_add_f64 %7, %5, %7\n\t"                 // t = w0 + t
+            "v_mul_f64 %7, -%7, %16\n\t"               // K0 = -t * il00
+            DPPFN("%0", "%6", "%6", 0) DPPFN("%1", "%6", "%6", 1) DPPFN("%2", "%6", "%6", 2)
+            DPPFN("%3", "%6", "%6", 3) DPPFN("%4", "%6", "%6", 4) DPPFN("%0", "%5", "%5", 0) DPPFN("%1", "%5", "%5", 1)
+            DPPFN("%2", "%5", "%5", 2) DPPFN("%3", "%5", "%5", 3) DPPFN("%4", "%5", "%5", 4)
+            : "+&v"(am[0]), "+&v"(am[1]), "+&v"(am[2]), "+&v"(am[3]), "+&v"(am[4]), "=&v"(w0), "=&v"(w1),
+              "=&v"(tt), "=&v"(K1)
+            : "v"(c0), "v"(v3), "v"(c2), "v"(c1), "v"(v4), "v"(il11), "v"(l10), "v"(il00));
+        K0 = tt;
+    } else
+#endif
+    {
+        w0 = c0 * v3;
+        w1 = fma(c1, v4, c2 * w0);
+        K1 = -w1 * il11;
+        K0 = -(w0 + l10 * K1) * il00;
+    }
     // K by rows (lane i writes column i); the Cholesky factor of S is group-uniform: all five lanes write
     // the same values
     S.KR[KRS * t + L.i] = K0;
@@ -627,6 +688,32 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
     S.Si[SIS * t + 1] = l10;
     S.Si[SIS * t + 2] = il11;
     if (upd) {
+#ifndef MPC_FAC_NOP
+        // P(i,j) = A'M(i,j) - W1_i W1_j - W0_i W0_j (done above) + Qt(i,j), then the symmetrisation below; the
+        // block forms P's rows and the kept upper entries first (the same additions and products as the
+        // MPC_FAC_NOP code), so each broadcast row is 5 or more instructions old: no s_nop
+        double sy0, sy1, sy2, sy3, p0, p1, p2, p4;
+        asm("v_add_f64 %5, %9, %13\n\t"                // p1 = am1 + q1
+            "v_add_f64 %6, %10, %14\n\t"               // p2 = am2 + q2
+            "v_add_f64 %7, %12, %15\n\t"               // p4 = am4 + q3
+            "v_add_f64 %4, %8, %16\n\t"                // p0 = am0 + q0
+            "v_mul_f64 %1, %5, %18\n\t"                // sy1 = p1 * k1
+            "v_mul_f64 %2, %6, %19\n\t"                // sy2 = p2 * k2
+            "v_mul_f64 %3, %11, %20\n\t"               // sy3 = am3 * k3
+            "v_mul_f64 %0, %4, %17\n\t"                // sy0 = p0 * k0
+            DPPF("%0", "%5", "%21", 0) DPPF("%1", "%6", "%22", 1) DPPF("%2", "%11", "%23", 2)
+            DPPF("%3", "%7", "%24", 3) DPPF("%0", "%6", "%22", 0) DPPF("%1", "%11", "%23", 1) DPPF("%2", "%7", "%24", 2)
+            DPPF("%0", "%11", "%23", 0) DPPF("%1", "%7", "%24", 1) DPPF("%0", "%7", "%24", 0)
+            : "=&v"(sy0), "=&v"(sy1), "=&v"(sy2), "=&v"(sy3), "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p4)
+            : "v"(am[0]), "v"(am[1]), "v"(am[2]), "v"(am[3]), "v"(am[4]), "v"(F.q[1]), "v"(F.q[2]), "v"(F.q[3]),
+              "v"(F.q[0]), "v"(L.k0), "v"(L.k1), "v"(L.k2), "v"(L.k3), "v"(L.r1), "v"(L.r2), "v"(L.r3), "v"(L.r4));
+        (void)p0;
+        pr[0] = sy0;
+        pr[1] = sy1;
+        pr[2] = sy2;
+        pr[3] = sy3;
+        pr[4] = p4;
+#else
         // P(i,j) = A'M(i,j) - W1_i W1_j - W0_i W0_j + Qt(i,j)
         asm("s_nop 1\n\t" DPPFN("%0", "%5", "%5", 0) DPPFN("%1", "%5", "%5", 1) DPPFN("%2", "%5", "%5", 2)
             DPPFN("%3", "%5", "%5", 3) DPPFN("%4", "%5", "%5", 4) DPPFN("%0", "%6", "%6", 0) DPPFN("%1", "%6", "%6", 1)
@@ -652,6 +739,7 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
         pr[1] = sy1;
         pr[2] = sy2;
         pr[3] = sy3;
+#endif
     }
 }
 // NT > 0: horizon fixed at compile time, stages fully unrolled (immediate LDS offsets, no loop control)
@@ -735,14 +823,30 @@ __device__ __forceinline__ void load_fwd(const Lds& S, const DLane& L, int t, Fw
     F.f4 = a5[L.of4];
 }
 // step t: p = p_{t+1} on entry (stored for phase 2), p_t on exit (t >= 1)
+// BX: the hazard-free block (dt K products first, no s_nop); the obstacle kernels use it (C3 -2.6%), the
+// obstacle-free N = 20 interior-point kernel keeps the s_nop form, whose register allocation it suits better
+// (C2: 0.3311-0.3323 ms against 0.3339-0.3344 with both changes, profiles/r06_ab_hazard.log)
+template <bool BX>
 __device__ __forceinline__ void bwd_step(const Lds& S, const DLane& L, int t, double dt, const BwdRec& B, double& p) {
     S.QR[QRS * (t + 1) + L.ps] = p;
     if (t >= 1) {
         double acc = fma(B.K0, B.g0, fma(B.K1, B.g1, B.qi));
+        if constexpr (!BX) {
         const double kd0 = B.K0 * dt, kd1 = B.K1 * dt;
         asm("s_nop 1\n\t" DPPF("%0", "%1", "%2", 3) DPPF("%0", "%1", "%3", 4) DPPF("%0", "%1", "%4", 2)
             DPPF("%0", "%1", "%5", 1) DPPF("%0", "%1", "%6", 0)
             : "+&v"(acc) : "v"(p), "v"(kd0), "v"(kd1), "v"(B.e2), "v"(B.e1), "v"(L.e0));
+        } else {
+        // the two products dt K(r, i) are the block's first two instructions: they are the two wait states the
+        // VALU-write -> DPP-read hazard on p needs (p was written by the previous step), so no s_nop
+        double kd0, kd1;
+        asm("v_mul_f64 %1, %7, %9\n\t"
+            "v_mul_f64 %2, %8, %9\n\t"
+            DPPF("%0", "%3", "%1", 3) DPPF("%0", "%3", "%2", 4) DPPF("%0", "%3", "%4", 2)
+            DPPF("%0", "%3", "%5", 1) DPPF("%0", "%3", "%6", 0)
+            : "+&v"(acc), "=&v"(kd0), "=&v"(kd1)
+            : "v"(p), "v"(B.e2), "v"(B.e1), "v"(L.e0), "v"(B.K0), "v"(B.K1), "v"(dt));
+        }
         p = acc + p;
     }
 }
@@ -829,7 +933,7 @@ __device__ __forceinline__ void fwd_step(const Lds& S, const DLane& L, int t, co
 }
 
 // NT > 0: the horizon is a compile-time constant and the recursions are fully unrolled.
-template <int NT>
+template <int NT, bool BX>
 __device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, int gl) {
     const DLane L = dlane(gl, dt);
     double p = S.QH[QHS * N + L.i];
@@ -845,7 +949,7 @@ __device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, 
             sched_fence();
             load_bwd(S, L, t >= 1 ? t - 1 : 0, buf[(NT - t) & 1]);
             sched_fence();
-            bwd_step(S, L, t, dt, buf[(NT - 1 - t) & 1], p);
+            bwd_step<BX>(S, L, t, dt, buf[(NT - 1 - t) & 1], p);
         }
     } else {
         BwdRec A, B;
@@ -855,12 +959,12 @@ __device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, 
             sched_fence();
             load_bwd(S, L, t >= 1 ? t - 1 : 0, B);
             sched_fence();
-            bwd_step(S, L, t, dt, A, p);
+            bwd_step<BX>(S, L, t, dt, A, p);
             if (--t < 0) break;
             sched_fence();
             load_bwd(S, L, t >= 1 ? t - 1 : 0, A);
             sched_fence();
-            bwd_step(S, L, t, dt, B, p);
+            bwd_step<BX>(S, L, t, dt, B, p);
             if (--t < 0) break;
         }
     }
@@ -936,11 +1040,12 @@ __device__ __forceinline__ void solve_fwd_lanes(const Lds& S, int N, double dt, 
     }
 }
 // the recursions run on lanes 0..4 of each group (exec narrowed), the stage phases on lanes 0..N-1.
-// ACL: the forward solve runs on closed-loop rows (built with kk) and u follows stage-parallel.
-template <int NT, bool ACL>
+// ACL: the forward solve runs on closed-loop rows (built with kk) and u follows stage-parallel.  BX: the
+// backward steps' hazard-free form (bwd_step).
+template <int NT, bool ACL, bool BX>
 __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
     const int N = NT > 0 ? NT : Nrt;
-    if (gl < 5) solve_bwd_lanes<NT>(S, N, dt, gl);
+    if (gl < 5) solve_bwd_lanes<NT, BX>(S, N, dt, gl);
     wave_sync();
     if (gl < N) {
         kk_stage(S, gl, dt);
@@ -1343,8 +1448,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             if (!xo_start) {
                 wave_sync();
                 riccati_factor<NT>(S, N, dt, gl);
-                if constexpr (ACL && GL == 64) riccati_solve<NTR, ACL>(S, N, dt, gl);
-                else riccati_solve<NTR, false>(S, N, dt, gl);
+                if constexpr (ACL && GL == 64) riccati_solve<NTR, ACL, OBS>(S, N, dt, gl);
+                else riccati_solve<NTR, false, OBS>(S, N, dt, gl);
             }
             if (MODE == MODE_IPM && cached) {
                 const double* xo = stc_in + stage_cache_xo(N) + 6 * (live ? k - 1 : 0);
@@ -1622,7 +1727,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 }
                 wave_sync();
                 PROF(6)
-                riccati_solve<NTR, ACL>(S, N, dt, gl);
+                riccati_solve<NTR, ACL, OBS>(S, N, dt, gl);
                 PROF(7)
                 // row directions and the largest feasible step
                 double dx4[4];
@@ -1846,8 +1951,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     // (G >= 2): the MODE_XO launch has no AC rows (lite LDS layout), and MODE_FULL must give
                     // bit-identical results.  GL = 64 (G = 1) is never split and keeps the AC rows (the
                     // K-row crossover cost C5 4%).
-                    if (ACL && (phase == 1 || GL == 64)) riccati_solve<NTR, ACL>(S, N, dt, gl);
-                    else riccati_solve<NTR, false>(S, N, dt, gl);
+                    if (ACL && (phase == 1 || GL == 64)) riccati_solve<NTR, ACL, OBS>(S, N, dt, gl);
+                    else riccati_solve<NTR, false, OBS>(S, N, dt, gl);
                     {
                         double dx4[4];
 #pragma unroll
