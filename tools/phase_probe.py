@@ -15,6 +15,7 @@ import __graft_entry__ as _ge
 # so the phase numbers never describe an older kernel
 _ge.build(prof=True)
 mpcqp.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcqp_prof.so")
+mpcqp._lib = None   # build() loaded the product library; load the twin instead
 L = mpcqp.lib()
 L.mpc_debug_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"

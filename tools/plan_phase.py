@@ -20,6 +20,7 @@ import __graft_entry__ as _ge
 # so the phase numbers never describe an older kernel
 _ge.build(prof=True)
 mpcplan.LIB_PATH = os.path.join(ROOT, "safe-autonomous-driving-mpc_amd", "libmpcplan_prof.so")
+mpcplan._lib = None   # build() loaded the product library; load the twin instead
 import workloads as W
 
 PHASES = ["TOTAL", "build_qp", "stage_hess", "factor", "solve", "ipm_rows", "eqp_rows", "multipliers",
