@@ -571,6 +571,11 @@ __device__ __forceinline__ void load_fac(const Lds& S, const DLane& L, int t, Fa
     ld2(S.QR + QRS * t + 4 * L.i, F.q[0], F.q[1]);
     ld2(S.QR + QRS * t + 4 * L.i + 2, F.q[2], F.q[3]);
 }
+// CF: the copy-free form (the A'M block reads p1, p3, p4 from its in-place accumulators, so pr[1], pr[3], pr[4]
+// need no register copies, and a bare pivot floor): 4 instructions fewer per stage, bit-identical.  The obstacle
+// kernels use it (C3 -0.7%); in the obstacle-free N = 20 interior-point kernel the same code measured +0.3%
+// (300-launch A/B), so it keeps the plain form
+template <bool CF>
 __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bool upd, double dt, double dt2,
                                          const FacRec& F, double pr[5]) {
     const double a12 = F.a[0], a14 = F.a[1], a20 = F.a[2], a23 = F.a[3], a24 = F.a[4];
@@ -580,7 +585,13 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
         : "+&v"(s00), "+&v"(s01), "+&v"(s11) : "v"(pr[3]), "v"(pr[4]), "v"(dt2));
     // pivot floors: never active in practice (s00 >= Rt >= 2 w_u1 > 0); a NaN pivot is floored too, the
     // NaN still reaches P and K through V and M
-    s00 = fmax(s00, 1e-300);
+    if constexpr (CF) {
+        // bare v_max_f64 (as vmax): fmax first quiets the asm result with a v_max_f64 x, x, x
+        const double floor_ = 1e-300;
+        asm("v_max_f64 %0, %0, %1" : "+v"(s00) : "s"(floor_));
+    } else {
+        s00 = fmax(s00, 1e-300);
+    }
     const double il00 = frsqrt(s00), l10 = s01 * il00;
     const double r11 = fmax(s11 - l10 * l10, 1e-14 * s11);
     const double il11 = frsqrt(r11);
@@ -612,6 +623,7 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
         // written at least 2 instructions earlier inside the block (m[0] 5 before the first broadcast, m[4]
         // 4 before its own), and whatever the compiler wrote before the block is 6 or more instructions back.
         m[1] = pr[1];
+        if constexpr (!CF) {
         asm("v_fma_f64 %0, %10, %13, %11\n\t"          // m0 = fma(p2, a20, p0)
             "v_fma_f64 %2, %12, %14, %10\n\t"          // m2 = fma(p1, a12, p2)
             "v_fma_f64 %3, %10, %15, %16\n\t"          // m3 = fma(p2, a23, p3)
@@ -627,6 +639,25 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
             : "=&v"(m[0]), "+&v"(m[1]), "=&v"(m[2]), "=&v"(m[3]), "=&v"(m[4]), "+&v"(v3), "+&v"(v4)
             : "v"(L.e0), "v"(F.e2), "v"(F.e1), "v"(pr[2]), "v"(pr[0]), "v"(pr[1]),
               "v"(a20), "v"(a12), "v"(a23), "v"(pr[3]), "v"(a24), "v"(pr[4]), "v"(a14), "v"(dt));
+        } else {
+        // p1, p3, p4 are read from the in-place accumulators m1, v3, v4 themselves (they still hold them: the
+        // broadcasts come after the six fma()s), so pr[1], pr[3], pr[4] need no copies of their own
+        asm("v_fma_f64 %0, %10, %12, %11\n\t"          // m0 = fma(p2, a20, p0)
+            "v_fma_f64 %2, %1, %13, %10\n\t"           // m2 = fma(p1, a12, p2)
+            "v_fma_f64 %3, %10, %14, %5\n\t"           // m3 = fma(p2, a23, p3)
+            "v_fma_f64 %4, %10, %15, %6\n\t"           // t = fma(p2, a24, p4)
+            "v_fma_f64 %4, %1, %16, %4\n\t"            // t = fma(p1, a14, t)
+            "v_fma_f64 %4, %11, %17, %4\n\t"           // m4 = fma(p0, dt, t)
+            DPPF("%0", "%0", "%7", 0) DPPF("%1", "%1", "%7", 0) DPPF("%2", "%2", "%7", 0) DPPF("%3", "%3", "%7", 0)
+            DPPF("%4", "%4", "%7", 0) DPPF("%5", "%5", "%7", 0) DPPF("%6", "%6", "%7", 0)
+            DPPF("%0", "%0", "%8", 2) DPPF("%1", "%1", "%8", 2) DPPF("%2", "%2", "%8", 2) DPPF("%3", "%3", "%8", 2)
+            DPPF("%4", "%4", "%8", 2) DPPF("%5", "%5", "%8", 2) DPPF("%6", "%6", "%8", 2)
+            DPPF("%0", "%0", "%9", 1) DPPF("%1", "%1", "%9", 1) DPPF("%2", "%2", "%9", 1) DPPF("%3", "%3", "%9", 1)
+            DPPF("%4", "%4", "%9", 1) DPPF("%5", "%5", "%9", 1) DPPF("%6", "%6", "%9", 1)
+            : "=&v"(m[0]), "+&v"(m[1]), "=&v"(m[2]), "=&v"(m[3]), "=&v"(m[4]), "+&v"(v3), "+&v"(v4)
+            : "v"(L.e0), "v"(F.e2), "v"(F.e1), "v"(pr[2]), "v"(pr[0]),
+              "v"(a20), "v"(a12), "v"(a23), "v"(a24), "v"(a14), "v"(dt));
+        }
     } else {
         asm("s_nop 1\n\t" DPPF("%0", "%0", "%2", 0) DPPF("%1", "%1", "%2", 0) "s_nop 1\n\t"
             DPPF("%0", "%0", "%3", 2) DPPF("%1", "%1", "%3", 2) "s_nop 1\n\t"
@@ -743,7 +774,7 @@ __device__ __forceinline__ void fac_step(const Lds& S, const DLane& L, int t, bo
     }
 }
 // NT > 0: horizon fixed at compile time, stages fully unrolled (immediate LDS offsets, no loop control)
-template <int NT>
+template <int NT, bool CF>
 __device__ __forceinline__ void riccati_factor_lanes(const Lds& S, int Nrt, double dt, int gl) {
     const int N = NT > 0 ? NT : Nrt;
     const DLane L = dlane(gl, dt);
@@ -764,7 +795,7 @@ __device__ __forceinline__ void riccati_factor_lanes(const Lds& S, int Nrt, doub
             lds_fence();
             load_fac(S, L, t >= 1 ? t - 1 : 0, buf[(NT - t) & 1]);
             sched_fence();
-            fac_step(S, L, t, t >= 1, dt, dt2, buf[(NT - 1 - t) & 1], pr);
+            fac_step<CF>(S, L, t, t >= 1, dt, dt2, buf[(NT - 1 - t) & 1], pr);
         }
     } else {
         FacRec A, B;
@@ -774,21 +805,21 @@ __device__ __forceinline__ void riccati_factor_lanes(const Lds& S, int Nrt, doub
             lds_fence();
             load_fac(S, L, t >= 1 ? t - 1 : 0, B);      // unconditional: keeps the LDS wait counts exact
             sched_fence();
-            fac_step(S, L, t, t >= 1, dt, dt2, A, pr);
+            fac_step<CF>(S, L, t, t >= 1, dt, dt2, A, pr);
             if (--t < 0) break;
             lds_fence();
             load_fac(S, L, t >= 1 ? t - 1 : 0, A);
             sched_fence();
-            fac_step(S, L, t, t >= 1, dt, dt2, B, pr);
+            fac_step<CF>(S, L, t, t >= 1, dt, dt2, B, pr);
             if (--t < 0) break;
         }
     }
 }
 // the recursion runs on lanes 0..4 of each group only (exec narrowed): the other lanes would compute
 // discarded values, and with them out of exec every store is a plain store
-template <int NT>
+template <int NT, bool CF>
 __device__ void riccati_factor(const Lds& S, int Nrt, double dt, int gl) {
-    if (gl < 5) riccati_factor_lanes<NT>(S, Nrt, dt, gl);
+    if (gl < 5) riccati_factor_lanes<NT, CF>(S, Nrt, dt, gl);
     wave_sync();
 }
 
@@ -1193,6 +1224,14 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
     // row right-hand sides recomputed after the solve (WRC) instead of held live across it: obstacle
     // kernels only (measured neutral on the obstacle-free N = 20 kernel)
     constexpr bool WRC = OBS;
+    // the factorisation's copy-free A'M block (fac_step): obstacle kernels only (see fac_step)
+#if defined(MPC_FAC_CF_NONE)
+    constexpr bool FAC_CF = false;
+#elif defined(MPC_FAC_CF_ALL)
+    constexpr bool FAC_CF = true;
+#else
+    constexpr bool FAC_CF = OBS;
+#endif
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int ln = threadIdx.x;
     const int grp = ln / GL, gl = ln % GL;
@@ -1447,7 +1486,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             }
             if (!xo_start) {
                 wave_sync();
-                riccati_factor<NT>(S, N, dt, gl);
+                riccati_factor<NT, FAC_CF>(S, N, dt, gl);
                 if constexpr (ACL && GL == 64) riccati_solve<NTR, ACL, OBS>(S, N, dt, gl);
                 else riccati_solve<NTR, false, OBS>(S, N, dt, gl);
             }
@@ -1641,7 +1680,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             }
             wave_sync();
             PROF(4)
-            riccati_factor<NT>(S, N, dt, gl);
+            riccati_factor<NT, FAC_CF>(S, N, dt, gl);
             PROF(5)
             // -- predictor, corrector (and, if needed, centred) solves ---------------------------------
             double p4v[NR], p5v[NR], pbv[NBOX];
@@ -1901,7 +1940,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     S.Rt[2 * (k - 1) + 1] = R1 + (clb[2] + clb[3]) * (1.0 / POLISH_DELTA);
                 }
                 wave_sync();
-                riccati_factor<NT>(S, N, dt, gl);
+                riccati_factor<NT, FAC_CF>(S, N, dt, gl);
                 double xp[4] = {x4[0], x4[1], x4[2], x4[3]};
                 pu0 = du0;
                 pu1 = du1;
