@@ -225,6 +225,9 @@ def main():
             "config": {"workload": f"{args.config}: trajectory{wb['traj']}.json, N={N}, batch={B} egos per GPU, "
                                    f"max_obs={mo}, seed {cfg['seed']} (SURVEY 8d)", "global_batch": world * B,
                        "horizon": N, "parallelism": f"dp{world} (ego shards)"},
+            "comm": {"transport": comm.transport,
+                     "note": "the ranks' one exchange (barrier, max-over-ranks time, telemetry gather): 'rccl' = "
+                             "libmpcqp's communicator (mpc_comm_*), 'local' = world 1, 'gloo' = the CPU stand-in"},
             "solver": tel,
             "roofline": {"bound": "fp64-valu", "achieved": flops / avg_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": flops / avg_launch_s / 1e12 / FP64_PEAK_TFLOPS,
