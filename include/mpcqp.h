@@ -123,8 +123,8 @@ int mpc_solve_batch(mpc_ctx* c, int B, const double* x0, const double* obs, cons
  * once warmed up, no allocation (graph-capturable): the
  * two-phase work list is allocated by mpc_create for up to 2^20 instances (a larger B runs the
  * single-kernel path, same results).  The two-phase launch keeps, per deferred instance, its linearisation
- * point, nominal rollout and the crossover's solve (the interior point's start; 13N+5 doubles) in a stage
- * cache that grows on the first eager call with a larger B (hipMalloc, which waits for the device; at most
+ * point, nominal rollout, the crossover's solve (the interior point's start) and the trajectory lookups at
+ * its stages (21N+14 doubles for even N, 21N+13 for odd) in a stage cache that grows on the first eager call with a larger B (hipMalloc, which waits for the device; at most
  * 1 GiB, MPC_STAGE_CACHE=0 switches it off); a captured call never uses it (a later eager call may grow it,
  * which would leave the graph with a freed pointer) and recomputes the start bit for bit instead.  The work
  * list belongs to the context: consecutive eager calls on one context are ordered on the device even when
