@@ -140,7 +140,8 @@ class ShardComm:
         GPU index (RCCL), or None for the CPU stand-in (gloo)."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
-        if world == 1:
+        # MPC_COMM=rccl runs a world-1 GPU rank through the communicator too (the N > 1 code path on one GPU)
+        if world == 1 and not (device is not None and os.environ.get("MPC_COMM") == "rccl"):
             return cls(1, 0, "local")
         if device is None:
             import torch.distributed as dist
