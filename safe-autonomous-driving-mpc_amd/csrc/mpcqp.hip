@@ -861,20 +861,18 @@ __device__ __forceinline__ void load_fwd(const Lds& S, const DLane& L, int t, Fw
     F.f4 = a5[L.of4];
 }
 // step t: p = p_{t+1} on entry (stored for phase 2), p_t on exit (t >= 1)
-// BX: the hazard-free block (dt K products first, no s_nop); the obstacle kernels use it (C3 -2.6%), the
-// obstacle-free N = 20 interior-point kernel keeps the s_nop form, whose register allocation it suits better
-// (C2: 0.3311-0.3323 ms against 0.3339-0.3344 with both changes, profiles/r06_ab_hazard.log)
-template <bool BX>
+// The hazard-free block (dt K products first, no s_nop): C3 -2.6% (profiles/r06_ab_hazard.log); in every kernel
+// since the stage lookups (C2 -0.1..-0.3%, profiles/r06_ab_bwd_all.log).  -DMPC_BWD_NOP: the s_nop form.
 __device__ __forceinline__ void bwd_step(const Lds& S, const DLane& L, int t, double dt, const BwdRec& B, double& p) {
     S.QR[QRS * (t + 1) + L.ps] = p;
     if (t >= 1) {
         double acc = fma(B.K0, B.g0, fma(B.K1, B.g1, B.qi));
-        if constexpr (!BX) {
+#ifdef MPC_BWD_NOP
         const double kd0 = B.K0 * dt, kd1 = B.K1 * dt;
         asm("s_nop 1\n\t" DPPF("%0", "%1", "%2", 3) DPPF("%0", "%1", "%3", 4) DPPF("%0", "%1", "%4", 2)
             DPPF("%0", "%1", "%5", 1) DPPF("%0", "%1", "%6", 0)
             : "+&v"(acc) : "v"(p), "v"(kd0), "v"(kd1), "v"(B.e2), "v"(B.e1), "v"(L.e0));
-        } else {
+#else
         // the two products dt K(r, i) are the block's first two instructions: they are the two wait states the
         // VALU-write -> DPP-read hazard on p needs (p was written by the previous step), so no s_nop
         double kd0, kd1;
@@ -884,7 +882,7 @@ __device__ __forceinline__ void bwd_step(const Lds& S, const DLane& L, int t, do
             DPPF("%0", "%3", "%5", 1) DPPF("%0", "%3", "%6", 0)
             : "+&v"(acc), "=&v"(kd0), "=&v"(kd1)
             : "v"(p), "v"(B.e2), "v"(B.e1), "v"(L.e0), "v"(B.K0), "v"(B.K1), "v"(dt));
-        }
+#endif
         p = acc + p;
     }
 }
@@ -971,7 +969,7 @@ __device__ __forceinline__ void fwd_step(const Lds& S, const DLane& L, int t, co
 }
 
 // NT > 0: the horizon is a compile-time constant and the recursions are fully unrolled.
-template <int NT, bool BX>
+template <int NT>
 __device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, int gl) {
     const DLane L = dlane(gl, dt);
     double p = S.QH[QHS * N + L.i];
@@ -987,7 +985,7 @@ __device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, 
             sched_fence();
             load_bwd(S, L, t >= 1 ? t - 1 : 0, buf[(NT - t) & 1]);
             sched_fence();
-            bwd_step<BX>(S, L, t, dt, buf[(NT - 1 - t) & 1], p);
+            bwd_step(S, L, t, dt, buf[(NT - 1 - t) & 1], p);
         }
     } else {
         BwdRec A, B;
@@ -997,12 +995,12 @@ __device__ __forceinline__ void solve_bwd_lanes(const Lds& S, int N, double dt, 
             sched_fence();
             load_bwd(S, L, t >= 1 ? t - 1 : 0, B);
             sched_fence();
-            bwd_step<BX>(S, L, t, dt, A, p);
+            bwd_step(S, L, t, dt, A, p);
             if (--t < 0) break;
             sched_fence();
             load_bwd(S, L, t >= 1 ? t - 1 : 0, A);
             sched_fence();
-            bwd_step<BX>(S, L, t, dt, B, p);
+            bwd_step(S, L, t, dt, B, p);
             if (--t < 0) break;
         }
     }
@@ -1078,12 +1076,11 @@ __device__ __forceinline__ void solve_fwd_lanes(const Lds& S, int N, double dt, 
     }
 }
 // the recursions run on lanes 0..4 of each group (exec narrowed), the stage phases on lanes 0..N-1.
-// ACL: the forward solve runs on closed-loop rows (built with kk) and u follows stage-parallel.  BX: the
-// backward steps' hazard-free form (bwd_step).
-template <int NT, bool ACL, bool BX>
+// ACL: the forward solve runs on closed-loop rows (built with kk) and u follows stage-parallel.
+template <int NT, bool ACL>
 __device__ void riccati_solve(const Lds& S, int Nrt, double dt, int gl) {
     const int N = NT > 0 ? NT : Nrt;
-    if (gl < 5) solve_bwd_lanes<NT, BX>(S, N, dt, gl);
+    if (gl < 5) solve_bwd_lanes<NT>(S, N, dt, gl);
     wave_sync();
     if (gl < N) {
         kk_stage(S, gl, dt);
@@ -1508,8 +1505,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
             if (!xo_start) {
                 wave_sync();
                 riccati_factor<NT, FAC_CF>(S, N, dt, gl);
-                if constexpr (ACL && GL == 64) riccati_solve<NTR, ACL, OBS>(S, N, dt, gl);
-                else riccati_solve<NTR, false, OBS>(S, N, dt, gl);
+                if constexpr (ACL && GL == 64) riccati_solve<NTR, ACL>(S, N, dt, gl);
+                else riccati_solve<NTR, false>(S, N, dt, gl);
             }
             if (MODE == MODE_IPM && cached) {
                 const double* xo = stc_in + stage_cache_xo(N) + 6 * (live ? k - 1 : 0);
@@ -1787,7 +1784,7 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                 }
                 wave_sync();
                 PROF(6)
-                riccati_solve<NTR, ACL, OBS>(S, N, dt, gl);
+                riccati_solve<NTR, ACL>(S, N, dt, gl);
                 PROF(7)
                 // row directions and the largest feasible step
                 double dx4[4];
@@ -2011,8 +2008,8 @@ mpc_solve_kernel(DevTable tab, KParams Pr, int B, const double* __restrict__ x0g
                     // (G >= 2): the MODE_XO launch has no AC rows (lite LDS layout), and MODE_FULL must give
                     // bit-identical results.  GL = 64 (G = 1) is never split and keeps the AC rows (the
                     // K-row crossover cost C5 4%).
-                    if (ACL && (phase == 1 || GL == 64)) riccati_solve<NTR, ACL, OBS>(S, N, dt, gl);
-                    else riccati_solve<NTR, false, OBS>(S, N, dt, gl);
+                    if (ACL && (phase == 1 || GL == 64)) riccati_solve<NTR, ACL>(S, N, dt, gl);
+                    else riccati_solve<NTR, false>(S, N, dt, gl);
                     {
                         double dx4[4];
 #pragma unroll

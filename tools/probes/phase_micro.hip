@@ -41,16 +41,16 @@ __global__ void __launch_bounds__(64) probe(long long* cyc, double* out) {
     long long t0, t1, acc_f = 0, acc_s = 0, acc_b = 0, acc_k = 0, acc_w = 0, acc_u = 0;
     for (int r = 0; r < REP; ++r) {
         t0 = __builtin_amdgcn_s_memtime();
-        riccati_factor<NTP>(S, N, dt, gl);
+        riccati_factor<NTP, false>(S, N, dt, gl);
         t1 = __builtin_amdgcn_s_memtime();
         acc_f += t1 - t0;
         t0 = __builtin_amdgcn_s_memtime();
-        riccati_solve<NTP, ACL, false>(S, N, dt, gl);
+        riccati_solve<NTP, ACL>(S, N, dt, gl);
         t1 = __builtin_amdgcn_s_memtime();
         acc_s += t1 - t0;
         // the solve's phases one by one
         t0 = __builtin_amdgcn_s_memtime();
-        if (gl < 5) solve_bwd_lanes<NTP, false>(S, N, dt, gl);
+        if (gl < 5) solve_bwd_lanes<NTP>(S, N, dt, gl);
         wave_sync();
         t1 = __builtin_amdgcn_s_memtime();
         acc_b += t1 - t0;
