@@ -622,6 +622,7 @@ def plan_leg(B, steps, route_name, comm, dev, cpu_s, with_cpu):
                "note": "HIP events on the timing stream, which joins the side streams that run one launch per "
                        "residency class of horizons; inputs resident in HBM"}
         if with_cpu:
+            out["cpu_backend"] = plan_cpu_backend(r, wb, min(cpu_s, 5.0))
             out["cpu_baseline"], out["parity_sample"] = plan_cpu_baseline(r, wb, cpu_s, status, groups)
             out["cpu_reference"] = plan_cpu_reference(r, wb)
     pl.close()
@@ -668,6 +669,33 @@ def plan_fleet(B, device):
             "note": "wall time of the whole receding-horizon loop for every plan, the loop on the device "
                     "(plan_optimize_device: every plan on its own wavefront, no barrier across plans), plans "
                     "assembled on the host"}
+
+
+def plan_cpu_backend(route, wb, budget_s):
+    """libmpcplan's own host backend (plan_create(..., device = -1): csrc/plan_host.h on std::thread workers) on
+    the CPU share, on the same bounded sample of chunks as the oracle baseline."""
+    import numpy as np
+    import mpcplan
+    hw, full, threads = cpu_threads()
+    B = wb["x0"].shape[0]
+    n = min(B, max(256, 16 * threads))
+    idx = np.linspace(0, B - 1, n).astype(int)
+    old = os.environ.get("PLAN_CPU_THREADS")
+    os.environ["PLAN_CPU_THREADS"] = str(threads)          # read by plan_create
+    try:
+        pl = mpcplan.Planner(route, mpcplan.default_params(N=int(wb["N"].max())), device=-1)
+    finally:
+        if old is None:
+            os.environ.pop("PLAN_CPU_THREADS", None)
+        else:
+            os.environ["PLAN_CPU_THREADS"] = old
+    args = (wb["x0"][idx], wb["s_target"][idx], wb["is_final"][idx], wb["N"][idx])
+    done, dt = _timed_rate(lambda: pl.solve_chunks(*args), n, budget_s)
+    pl.close()
+    return {"value": done / dt, "unit": "chunks/s", "cores": threads,
+            "scope": "this process's CPU share of the GPU box (cgroup quota)",
+            "sample": f"{n} chunks spread over the batch, solved repeatedly for {dt:.1f} s by libmpcplan's host "
+                      f"backend (device = -1), {threads} threads"}
 
 
 def plan_cpu_baseline(route, wb, budget_s, status, groups):

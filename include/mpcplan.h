@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCPLAN_VERSION 2
+#define MPCPLAN_VERSION 3     /* 3: the host backend (device = -1) */
 #define PLAN_MAX_N 64          /* collocation intervals per chunk */
 
 /* status[] codes */
@@ -79,7 +79,12 @@ void plan_default_params(plan_params* p);
  *   cx, cy      [M-1][4] coefficients of the parametric CubicSpline x(t), y(t) over t = 0..M-1
  *               (path_planning.create_spline), scipy PPoly order: row i holds c[0..3, i], the cubic first;
  *   vmax[M]     speed limit at each way-point in m/s (:464-467).
- * device >= 0: HIP device index; there is no host backend (the CPU restatement is test infrastructure). */
+ * device >= 0: HIP device index.  device = -1: the host backend (csrc/plan_host.h): the same chunk algorithm in
+ * IEEE double on std::thread workers (PLAN_CPU_THREADS, default every hardware thread), no HIP call; it serves
+ * plan_solve_chunks, plan_optimize (the chunk loop on the CPU, one plan per worker), plan_route_eval,
+ * plan_set_params and plan_destroy, and the device-pointer entries (plan_solve_chunks_device,
+ * plan_optimize_device, plan_chunks_per_cu) fail on it with PLAN_E_DEVICE.  The reference's planner is CPU
+ * code (scipy SLSQP, :381-387); this is the library's CPU path behind the same entries. */
 int plan_create(const double* s, int M, const double* cx, const double* cy, const double* vmax,
                 const plan_params* p, int device, plan_ctx** out);
 
@@ -137,12 +142,14 @@ int plan_optimize_device(plan_ctx* c, int B, int Nmax, const double* starts, dou
 
 /* plan_optimize_device with host buffers, synchronous (inputs staged, outputs copied back): the same
  * arguments and outputs, slot = b * max_chunks + n.  Lets a host caller run the device chunk loop without a
- * device allocator of its own. */
+ * device allocator of its own.  On a host context (device = -1) the loop runs on the CPU, one plan per worker
+ * (the same chunk sequence and outputs). */
 int plan_optimize(plan_ctx* c, int B, int Nmax, const double* starts, double max_chunk_size, int max_chunks,
                   const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final, int* status,
                   int* iters, int* sqp, int* nchunks);
 
-/* Route functions on the device, for tests: kappa(s) and dkappa/ds (k_ref_fun, :445-459), v_max(s). */
+/* Route functions, for tests: kappa(s) and dkappa/ds (k_ref_fun, :445-459), v_max(s); on the device, or on the
+ * CPU for a host context. */
 int plan_route_eval(plan_ctx* c, int n, const double* s, double* kappa, double* dkappa, double* vmax);
 
 int plan_set_params(plan_ctx* c, const plan_params* p);

@@ -26,11 +26,13 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 
 #include "../../include/mpcplan.h"
 #include "plan_kernel.h"
+#include "plan_host.h"
 
 namespace {
 
@@ -48,6 +50,8 @@ size_t lds_bytes(int Nmax) { return sizeof(double) * (size_t)make_layout(Nmax).t
 struct plan_ctx {
     int device;
     plan_params p;
+    plan_host::route* host;   // device = -1: the host backend's route (plan_host.h); every HIP member unused
+    int host_threads;
     DevRoute R;
     double* d_route;          // s | cx | cy | vmax
     size_t lds_max;           // the device's LDS per workgroup
@@ -157,9 +161,24 @@ int plan_create(const double* s, int M, const double* cx, const double* cy, cons
     for (int i = 0; i < M; ++i)
         if (!std::isfinite(vmax[i])) return fail(PLAN_E_ARG, "speed limits must be finite");
     if (int rc = check_params(p)) return rc;
+    if (device == -1) {
+        // host backend: the chunk solve on std::thread workers (plan_host.h), no HIP call
+        plan_ctx* c = new plan_ctx();
+        c->device = -1;
+        c->p = *p;
+        if (plan_host::route_create(s, M, cx, cy, vmax, &c->host) != PLAN_SUCCESS) {
+            delete c;
+            return fail(PLAN_E_ALLOC, "host route allocation failed");
+        }
+        const char* te = std::getenv("PLAN_CPU_THREADS");
+        const int hw = (int)std::thread::hardware_concurrency();
+        c->host_threads = te && std::atoi(te) > 0 ? std::atoi(te) : std::max(1, hw);
+        *out = c;
+        return PLAN_SUCCESS;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PLAN_E_DEVICE, "no HIP device");
-    if (device < 0 || device >= ndev) return fail(PLAN_E_DEVICE, "device index out of range (there is no host backend)");
+    if (device < 0 || device >= ndev) return fail(PLAN_E_DEVICE, "device index out of range (-1: the host backend)");
     if (hipSetDevice(device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");
     int lds = 0;
     if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess) lds = 65536;
@@ -213,6 +232,11 @@ int plan_set_params(plan_ctx* c, const plan_params* p) {
 
 void plan_destroy(plan_ctx* c) {
     if (!c) return;
+    if (c->host) {
+        plan_host::route_destroy(c->host);
+        delete c;
+        return;
+    }
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     if (c->d_route) (void)hipFree(c->d_route);
@@ -228,6 +252,7 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
                              const int* is_final, double* X, double* U, double* S, int* status, int* iters, int* sqp,
                              void* stream) {
     if (!c) return fail(PLAN_E_ARG, "ctx is NULL");
+    if (c->host) return fail(PLAN_E_DEVICE, "plan_solve_chunks_device on a host context (device = -1): use plan_solve_chunks");
     if (B < 0) return fail(PLAN_E_ARG, "B must be >= 0");
     if (B == 0) return PLAN_SUCCESS;
     if (!x0 || !s_target) return fail(PLAN_E_ARG, "x0 and s_target are required");
@@ -293,6 +318,7 @@ int plan_solve_chunks_device(plan_ctx* c, int B, int Nmax, const int* N, const d
 
 int plan_chunks_per_cu(plan_ctx* c, int Nmax, int* out) {
     if (!c || !out) return fail(PLAN_E_ARG, "ctx and out are required");
+    if (c->host) return fail(PLAN_E_DEVICE, "plan_chunks_per_cu on a host context (device = -1)");
     if (Nmax < 1 || Nmax > PLAN_MAX_N) return fail(PLAN_E_ARG, "Nmax out of range [1, PLAN_MAX_N]");
     const size_t lds = lds_bytes(Nmax);
     if (lds > c->lds_max) return fail(PLAN_E_ARG, "Nmax too large for the device's LDS");
@@ -312,6 +338,7 @@ int plan_optimize_device(plan_ctx* c, int B, int Nmax, const double* starts, dou
                          const double* avg, int nav, double* X, double* U, double* S, int* N, int* is_final,
                          int* status, int* iters, int* sqp, int* nchunks, void* stream) {
     if (!c) return fail(PLAN_E_ARG, "ctx is NULL");
+    if (c->host) return fail(PLAN_E_DEVICE, "plan_optimize_device on a host context (device = -1): use plan_optimize");
     if (B < 0) return fail(PLAN_E_ARG, "B must be >= 0");
     if (B == 0) return PLAN_SUCCESS;
     if (!starts || !avg || !X || !U || !S || !N || !is_final || !status || !iters || !sqp || !nchunks)
@@ -365,6 +392,10 @@ int plan_solve_chunks(plan_ctx* c, int B, const int* N, const double* x0, const 
             Nmax = std::max(Nmax, N[b]);
         }
     }
+    if (c->host) {
+        plan_host::batch(c->host, &c->p, B, Nmax, N, x0, s_target, is_final, X, U, S, status, iters, sqp, c->host_threads);
+        return PLAN_SUCCESS;
+    }
     if (hipSetDevice(c->device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");
     const size_t nX = (size_t)B * (Nmax + 1) * 5, nU = (size_t)B * Nmax * 2, nS = (size_t)B * Nmax;
     const size_t bytes = sizeof(double) * (5 * (size_t)B + B + nX + nU + nS) + sizeof(int) * (5 * (size_t)B);
@@ -416,6 +447,12 @@ int plan_optimize(plan_ctx* c, int B, int Nmax, const double* starts, double max
     if (Nmax < 1 || Nmax > PLAN_MAX_N) return fail(PLAN_E_ARG, "Nmax out of range [1, PLAN_MAX_N]");
     if (max_chunks < 1) return fail(PLAN_E_ARG, "max_chunks must be >= 1");
     if (nav < 1) return fail(PLAN_E_ARG, "avg must have at least one entry");
+    if (c->host) {
+        if (!(max_chunk_size > 0.0) || !std::isfinite(max_chunk_size)) return fail(PLAN_E_ARG, "max_chunk_size must be > 0");
+        plan_host::optimize(c->host, &c->p, B, Nmax, starts, max_chunk_size, max_chunks, avg, nav, X, U, S, N, is_final,
+                            status, iters, sqp, nchunks, c->host_threads);
+        return PLAN_SUCCESS;
+    }
     if (hipSetDevice(c->device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");
     const size_t slots = (size_t)B * max_chunks;
     const size_t nX = slots * (Nmax + 1) * 5, nU = slots * Nmax * 2, nS = slots * Nmax;
@@ -463,6 +500,13 @@ int plan_route_eval(plan_ctx* c, int n, const double* s, double* kappa, double* 
     if (!c) return fail(PLAN_E_ARG, "ctx is NULL");
     if (n < 0 || (n > 0 && (!s || !kappa || !dkappa || !vmax))) return fail(PLAN_E_ARG, "bad arguments");
     if (n == 0) return PLAN_SUCCESS;
+    if (c->host) {
+        for (int i = 0; i < n; ++i) {
+            kappa[i] = plan_host::route_kappa_at(c->host, s[i], &dkappa[i]);
+            vmax[i] = plan_host::route_vmax_at(c->host, s[i]);
+        }
+        return PLAN_SUCCESS;
+    }
     if (hipSetDevice(c->device) != hipSuccess) return fail(PLAN_E_DEVICE, "hipSetDevice failed");
     double* d = nullptr;
     if (hipMalloc(&d, sizeof(double) * 4 * (size_t)n) != hipSuccess) return fail(PLAN_E_ALLOC, "allocation failed");
