@@ -5,7 +5,9 @@ tests/asan/Makefile builds, with -fsanitize=address,undefined (every report fata
                  trajectory_loader.py:13-24), the device-table build (:26-84) and the bucketed interval
                  search restated from the device's seg_t;
   oracle_driver  oracle/mpc_oracle.c -- the CPU restatement;
-  cpu_driver     csrc/cpu_backend.h -- the product's host backend (mpc_create device = -1), on 3 threads.
+  cpu_driver     csrc/cpu_backend.h -- the product's host backend (mpc_create device = -1), on 3 threads;
+  plan_driver    csrc/plan_host.h -- libmpcplan's host backend (plan_create device = -1): a chunk batch and the
+                 receding-horizon loop, on 3 threads; equal bit for bit to the library's own host backend.
 The reader runs over the reference trajectories (regenerated from the package data, verbatim floats) and a
 malformed / duplicate-key / deeply nested corpus; every answer must match Python's json.load (the
 reference's loader).  Both solver drivers' results must equal the regular oracle build's bit for bit.
@@ -32,7 +34,8 @@ def drivers():
     with FileLock(os.path.join(ASAN, ".build.lock")):
         r = subprocess.run(["make", "-C", ASAN], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    return os.path.join(ASAN, "json_driver"), os.path.join(ASAN, "oracle_driver"), os.path.join(ASAN, "cpu_driver")
+    return (os.path.join(ASAN, "json_driver"), os.path.join(ASAN, "oracle_driver"), os.path.join(ASAN, "cpu_driver"),
+            os.path.join(ASAN, "plan_driver"))
 
 
 def traj_json(i):
@@ -164,3 +167,69 @@ def test_oracle_under_asan_matches_regular_build(drivers, tmp_path, kind, B, sqp
                          nob if mo else None)
     assert np.array_equal(sa, ro["status"])
     assert np.array_equal(Ua, ro["U"]) and np.array_equal(Xa, ro["Xpred"])
+
+
+def test_plan_host_backend_under_asan(drivers, tmp_path):
+    """csrc/plan_host.h under ASan/UBSan on 3 threads: 24 chunks of mixed horizons (intermediate and final) and
+    the chunk loop from 2 starts; every output equals libmpcplan's host backend (plan_create device = -1)."""
+    import __graft_entry__ as g
+    g.build()
+    import mpcplan
+    import workloads as W
+    r = W.plan_route("synth1")
+    rng = np.random.default_rng(4)
+    B, P, Cn = 24, 2, 40
+    s0 = rng.uniform(0.0, r.s_total - 45.0, B)
+    x0 = np.zeros((B, 5))
+    x0[:, 0] = s0
+    x0[:, 3] = [r.k_ref_fun(s) for s in s0]
+    x0[:, 4] = [0.6 * r.v_max_fun(s) for s in s0]
+    fin = (np.arange(B) % 3 == 2).astype(np.int32)
+    st = np.where(fin == 1, np.minimum(s0 + 35.0, r.s_total), s0 + 20.0)
+    N = np.array([(13, 17, 22)[i % 3] for i in range(B)], np.int32)
+    Nmax = 32
+    starts = np.zeros((P, 5))
+    starts[1] = (600.0, 0.0, 0.0, r.k_ref_fun(600.0), 0.5 * r.v_max_fun(600.0))
+    arr = [np.ascontiguousarray(a, np.float64) for a in (r.s, r.cx, r.cy, r.vmax)]
+    M = arr[0].size
+    avg = np.array([float(np.mean(arr[3][i:])) for i in range(M)])
+    fin_in, fout = tmp_path / "plan_in.bin", tmp_path / "plan_out.bin"
+    with open(fin_in, "wb") as f:
+        np.array([M, B, Nmax, P, Cn], np.int32).tofile(f)
+        for a in arr:
+            a.tofile(f)
+        N.tofile(f); fin.tofile(f); x0.tofile(f); st.tofile(f); starts.tofile(f); avg.tofile(f)
+    res = subprocess.run([drivers[3], str(fin_in), str(fout)], capture_output=True, text=True, env=ENV, timeout=900)
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert "runtime error" not in res.stderr and "AddressSanitizer" not in res.stderr, res.stderr[-3000:]
+    raw = open(fout, "rb").read()
+    off = 0
+
+    def take(dt, n):
+        nonlocal off
+        a = np.frombuffer(raw, dt, n, off)
+        off += a.nbytes
+        return a
+
+    X = take(np.float64, B * (Nmax + 1) * 5).reshape(B, Nmax + 1, 5)
+    U = take(np.float64, B * Nmax * 2).reshape(B, Nmax, 2)
+    S = take(np.float64, B * Nmax).reshape(B, Nmax)
+    status, iters, sqp = take(np.int32, B), take(np.int32, B), take(np.int32, B)
+    LX = take(np.float64, P * Cn * (Nmax + 1) * 5).reshape(P, Cn, Nmax + 1, 5)
+    LN, Lst, nch = take(np.int32, P * Cn).reshape(P, Cn), take(np.int32, P * Cn).reshape(P, Cn), take(np.int32, P)
+    pl = mpcplan.Planner(r, mpcplan.default_params(N=Nmax), device=-1)
+    # the library solves with the batch's own row stride (its largest horizon); compare on those rows
+    ref = pl.solve_chunks(x0, st, fin, N)
+    nm = int(N.max())
+    assert np.array_equal(X[:, :nm + 1], ref["X"]) and np.array_equal(U[:, :nm], ref["U"])
+    assert np.array_equal(S[:, :nm], ref["S"])
+    for a, b in ((status, ref["status"]), (iters, ref["iters"]), (sqp, ref["sqp"])):
+        assert np.array_equal(a, b)
+    lo = pl.optimize_device(starts, 20.0, Cn, avg, Nmax)
+    assert np.array_equal(nch, lo["nchunks"])
+    for b in range(P):
+        n = int(nch[b])
+        assert n > 0
+        assert np.array_equal(LN[b, :n], lo["N"][b, :n]) and np.array_equal(Lst[b, :n], lo["status"][b, :n])
+        assert np.array_equal(LX[b, :n], lo["X"][b, :n])
+    pl.close()
