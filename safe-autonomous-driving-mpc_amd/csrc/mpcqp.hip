@@ -946,11 +946,25 @@ __device__ __forceinline__ void load_acl(const Lds& S, const DLane& L, int t, Ac
     ld2(ac + 2, F.c[2], F.c[3]);
     ld2(ac + 4, F.c[4], F.d);
 }
-// x_{t+1}(i) = sum_m Acl_t(i,m) x_m + (B kk_t)_i: one chain of five broadcast FMAs
+// x_{t+1}(i) = sum_m Acl_t(i,m) x_m + (B kk_t)_i: one chain of five broadcast FMAs.
+// NOP: the s_nop 1 covering the VALU-write -> DPP-read hazard on x.  Only the first step needs it (x = 0 was
+// just materialised); in the unrolled recursions every later x is the previous chain's last FMA, followed by
+// its LDS store, the next record's loads and waits (tools/dpp_hazard_check.py checks the listing)
+template <bool NOP = true>
 __device__ __forceinline__ void acl_step(const Lds& S, const DLane& L, int t, AclRec& F, double& x) {
-    asm("s_nop 1\n\t" DPPF("%0", "%1", "%2", 0) DPPF("%0", "%1", "%3", 1) DPPF("%0", "%1", "%4", 2)
-        DPPF("%0", "%1", "%5", 3) DPPF("%0", "%1", "%6", 4)
-        : "+&v"(F.d) : "v"(x), "v"(F.c[0]), "v"(F.c[1]), "v"(F.c[2]), "v"(F.c[3]), "v"(F.c[4]));
+#ifdef MPC_ACL_NOP
+    constexpr bool P = true;
+#else
+    constexpr bool P = NOP;
+#endif
+    if constexpr (P)
+        asm("s_nop 1\n\t" DPPF("%0", "%1", "%2", 0) DPPF("%0", "%1", "%3", 1) DPPF("%0", "%1", "%4", 2)
+            DPPF("%0", "%1", "%5", 3) DPPF("%0", "%1", "%6", 4)
+            : "+&v"(F.d) : "v"(x), "v"(F.c[0]), "v"(F.c[1]), "v"(F.c[2]), "v"(F.c[3]), "v"(F.c[4]));
+    else
+        asm(DPPF("%0", "%1", "%2", 0) DPPF("%0", "%1", "%3", 1) DPPF("%0", "%1", "%4", 2)
+            DPPF("%0", "%1", "%5", 3) DPPF("%0", "%1", "%6", 4)
+            : "+&v"(F.d) : "v"(x), "v"(F.c[0]), "v"(F.c[1]), "v"(F.c[2]), "v"(F.c[3]), "v"(F.c[4]));
     x = F.d;
     S.dX[5 * (t + 1) + L.i] = x;
 }
@@ -1018,7 +1032,8 @@ __device__ __forceinline__ void solve_acl_lanes(const Lds& S, int N, double dt, 
             sched_fence();
             load_acl(S, L, t + 1 < NT ? t + 1 : t, buf[(t + 1) & 1]);
             sched_fence();
-            acl_step(S, L, t, buf[t & 1], x);
+            if (t == 0) acl_step<true>(S, L, t, buf[t & 1], x);
+            else acl_step<false>(S, L, t, buf[t & 1], x);
         }
     } else {
         AclRec A, B;
